@@ -1,0 +1,126 @@
+/*
+ * include/labsort.h -- C-ABI of liblabsort.so, the MI355X-native (gfx950) sort.
+ *
+ * Plain pointers and sizes only (no HIP or torch types): `stream` is a
+ * hipStream_t passed as void* (NULL = the null stream), device pointers come
+ * from hipMalloc / torch tensors.  Every function returns a LABSORT_* status.
+ *
+ * What each entry replaces in the reference (`Sord Radix y Merge/`):
+ *   labsort_sort_host      order_array(int*, int)               lab.cu:303-402, lab.h:9
+ *                          (host pointer in, sorted in place, synchronous)
+ *   labsort_sort_device    stages 1-3 of order_array between the H2D copy
+ *                          (lab.cu:321) and the D2H copy (lab.cu:397)
+ *   labsort_wave_tile_sort radix_sort_kernel (lab.cu:47-87): per-tile bit
+ *                          split with early exit, wave64 tiles instead of warp32
+ *   labsort_tile_sort      stage 1+2 of order_array (lab.cu:323-346): sorted
+ *                          runs of labsort_tile_keys() keys
+ *   labsort_merge_pass     stage 3 iteration (separators_kernel +
+ *                          merge_segments_kernel, lab.cu:358-391)
+ *   labsort_merge          deviceOrderedJoin (lab.cu:144-182) generalised to a
+ *                          diagonal range of merge(A,B); used by the multi-GPU
+ *                          merge-split exchange
+ *   labsort_histogram      the global digit count of letra.pdf's split (no
+ *                          counterpart kernel in lab.cu)
+ *   sort(int*, int)        the north_star's name for order_array
+ * The C++-linkage drop-ins order_array / order_with_trust live in lab.h.
+ */
+#ifndef LABSORT_H
+#define LABSORT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define LABSORT_OK 0
+#define LABSORT_ERR_ARG 1        /* bad argument (NULL, n too large, workspace too small) */
+#define LABSORT_ERR_HIP 2        /* a HIP runtime call failed: labsort_last_hip_error() */
+#define LABSORT_ERR_DEVICE 3     /* a kernel reported an internal error (bounded spin expired) */
+
+/* algorithms */
+#define LABSORT_ALGO_RADIX 0     /* LSD radix, 8-bit digits, onesweep passes (default) */
+#define LABSORT_ALGO_MERGE 1     /* LDS tile radix + merge-path merge passes */
+#define LABSORT_ALGO_RADIX1 2    /* LSD radix with 1-bit digits: letra.pdf's split, 32 passes */
+
+/* key types: how the 32-bit words are ordered */
+#define LABSORT_KEY_U32 0
+#define LABSORT_KEY_I32 1
+
+/* generator distributions (oracle/cpu_sort.cpp uses the same codes and formula) */
+#define LABSORT_DIST_U32 0
+#define LABSORT_DIST_U31 1
+#define LABSORT_DIST_MOD100 2
+#define LABSORT_DIST_MOD1000 3
+#define LABSORT_DIST_SORTED 4
+#define LABSORT_DIST_REVERSED 5
+#define LABSORT_DIST_CONST 6
+#define LABSORT_DIST_LOWBITS 7
+
+/* kernel classes for the timing hooks */
+#define LABSORT_K_HISTOGRAM 0
+#define LABSORT_K_ONESWEEP 1
+#define LABSORT_K_TILE_SORT 2
+#define LABSORT_K_MERGE 3
+#define LABSORT_K_PARTITION 4
+#define LABSORT_K_COUNT 5
+
+/* ---- library info ---- */
+const char *labsort_version(void);
+const char *labsort_error_string(int status);
+int labsort_last_hip_error(void);                 /* hipError_t of the last failure */
+const char *labsort_hip_error_string(int hip_error);
+size_t labsort_max_keys(int algo);                /* largest n a device sort accepts */
+size_t labsort_tile_keys(void);                   /* run length produced by labsort_tile_sort */
+size_t labsort_merge_tile_keys(void);             /* output keys per merge workgroup */
+
+/* ---- whole sorts ---- */
+/* Bytes of device workspace labsort_sort_device needs for n keys. */
+size_t labsort_workspace_bytes(size_t n, int algo);
+/* Sort n keys from d_in into d_out (d_in == d_out allowed: in place).
+ * Asynchronous on `stream`; no host synchronisation, graph-capturable. */
+int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, int algo, void *d_workspace,
+                        size_t workspace_bytes, void *stream);
+/* Host pointer in/out, synchronous: the order_array contract (lab.cu:303). */
+int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo);
+
+/* ---- building blocks (exposed for tests and the multi-GPU driver) ---- */
+/* Sort every 64-key tile of d_keys in place by 1-bit splits (ballot + mbcnt +
+ * ds_permute), stopping early once the tile is sorted: radix_sort_kernel's job. */
+int labsort_wave_tile_sort(void *d_keys, size_t n, int key_type, void *stream);
+/* Sort every labsort_tile_keys() tile of d_in into d_out (in place allowed). */
+int labsort_tile_sort(const void *d_in, void *d_out, size_t n, int key_type, void *stream);
+/* One merge pass: runs of `run` keys (power of two, >= labsort_merge_tile_keys()/2)
+ * pairwise merged into runs of 2*run.  d_part: >= labsort_merge_parts(n) words. */
+size_t labsort_merge_parts(size_t n);
+int labsort_merge_pass(const void *d_in, void *d_out, size_t n, size_t run, int key_type, uint32_t *d_part,
+                       void *stream);
+/* out[0 .. d1-d0) = elements d0 .. d1-1 of merge(A, B) (A before B on ties).
+ * d_part: >= labsort_merge_parts(d1-d0) words. */
+int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *d_out, size_t d0, size_t d1,
+                  int key_type, uint32_t *d_part, void *stream);
+/* d_hist[p * 2^bits + digit] += count of keys with that digit in pass p
+ * (p = 0 .. ceil(32/bits)-1); bits = 8 or 1.  d_hist must be zeroed by the caller. */
+int labsort_histogram(const void *d_keys, size_t n, int key_type, int bits, uint32_t *d_hist, void *stream);
+
+/* ---- utilities ---- */
+/* Counter-based generator, identical to oracle_fill: keys first..first+n-1. */
+int labsort_fill(void *d_out, size_t n, uint64_t seed, int dist, uint64_t param, uint64_t first, void *stream);
+/* *d_count += number of i with key[i] > key[i+1] (0 = sorted). */
+int labsort_count_descents(const void *d_keys, size_t n, int key_type, uint32_t *d_count, void *stream);
+
+/* ---- timing hooks (HIP events on the sort's stream) ---- */
+int labsort_timing_enable(int on);                /* clears accumulated times */
+/* After the stream has been synchronised: total ms and launch count of a
+ * kernel class (LABSORT_K_*) recorded since labsort_timing_enable(1). */
+int labsort_timing_read(int kernel_class, double *total_ms, long long *launches);
+
+/* ---- the north_star's entry name (the reference never defined it) ---- */
+void sort(int *in, int n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LABSORT_H */

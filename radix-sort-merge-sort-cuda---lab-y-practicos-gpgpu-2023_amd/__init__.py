@@ -1,0 +1,240 @@
+"""labsort -- MI355X-native (gfx950) integer sort behind the reference's order_array API.
+
+The product is the native library `liblabsort.so` (HIP kernels + C++ host
+orchestration, C-ABI in include/labsort.h).  This module is a thin ctypes view of
+it for Python callers, tests and bench.py:
+
+  order_array(a)          lab.h:9 / lab.cu:303  -- int32 numpy array sorted in place
+                          through the GPU (host pointer, synchronous)
+  order_with_trust(a)     lab.h:10 / lab.cu:404 -- thrust::sort on the host pointer
+  sort_device(...)        the device-pointer sort (keys already in HBM)
+  wave_tile_sort, tile_sort, merge_pass, merge, histogram  -- the building blocks
+
+There is no CPU fallback: if the shared library is missing this module raises
+at import, and every device call raises LabsortError on a failed status.
+The package directory name is not a Python identifier; import it with
+``importlib.import_module("radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd")``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblabsort.so")
+
+OK, ERR_ARG, ERR_HIP, ERR_DEVICE = 0, 1, 2, 3
+ALGO = {"radix": 0, "merge": 1, "radix1": 2}
+KEY = {"u32": 0, "i32": 1}
+DIST = {"u32": 0, "u31": 1, "mod100": 2, "mod1000": 3, "sorted": 4, "reversed": 5, "const": 6, "lowbits": 7}
+KCLASS = {"histogram": 0, "onesweep": 1, "tile_sort": 2, "merge": 3, "partition": 4}
+
+# exported symbols of include/labsort.h + lab.h (checked by tests/test_abi.py)
+C_SYMBOLS = [
+    "labsort_version", "labsort_error_string", "labsort_last_hip_error", "labsort_hip_error_string",
+    "labsort_max_keys", "labsort_tile_keys", "labsort_merge_tile_keys", "labsort_workspace_bytes",
+    "labsort_sort_device", "labsort_sort_host", "labsort_wave_tile_sort", "labsort_tile_sort",
+    "labsort_merge_parts", "labsort_merge_pass", "labsort_merge", "labsort_histogram", "labsort_fill",
+    "labsort_count_descents", "labsort_timing_enable", "labsort_timing_read", "sort",
+]
+CXX_SYMBOLS = ["_Z11order_arrayPii", "_Z16order_with_trustPii"]
+
+
+class LabsortError(RuntimeError):
+    pass
+
+
+def _load() -> ctypes.CDLL:
+    # One HIP runtime per process: torch ships its own libamdhip64.so (SONAME
+    # libamdhip64.so.7).  Loading torch first makes liblabsort's DT_NEEDED
+    # libamdhip64.so.7 bind to that already-loaded runtime, so torch tensors and
+    # our kernels share one device context.  Loaded the other way round, a second
+    # runtime would come up and find no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the labsort path has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    p, sz, i, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_uint64
+    L.labsort_version.restype = ctypes.c_char_p
+    L.labsort_error_string.restype = ctypes.c_char_p
+    L.labsort_error_string.argtypes = [i]
+    L.labsort_hip_error_string.restype = ctypes.c_char_p
+    L.labsort_hip_error_string.argtypes = [i]
+    for f in ("labsort_max_keys", "labsort_workspace_bytes"):
+        getattr(L, f).restype = sz
+    L.labsort_max_keys.argtypes = [i]
+    L.labsort_tile_keys.restype = sz
+    L.labsort_merge_tile_keys.restype = sz
+    L.labsort_merge_parts.restype = sz
+    L.labsort_merge_parts.argtypes = [sz]
+    L.labsort_workspace_bytes.argtypes = [sz, i]
+    L.labsort_sort_device.argtypes = [p, p, sz, i, i, p, sz, p]
+    L.labsort_sort_host.argtypes = [p, sz, i, i]
+    L.labsort_wave_tile_sort.argtypes = [p, sz, i, p]
+    L.labsort_tile_sort.argtypes = [p, p, sz, i, p]
+    L.labsort_merge_pass.argtypes = [p, p, sz, sz, i, p, p]
+    L.labsort_merge.argtypes = [p, sz, p, sz, p, sz, sz, i, p, p]
+    L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
+    L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
+    L.labsort_count_descents.argtypes = [p, sz, i, p, p]
+    L.labsort_timing_enable.argtypes = [i]
+    L.labsort_timing_read.argtypes = [i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
+    L.sort.argtypes = [p, i]
+    L.sort.restype = None
+    fn = getattr(L, "_Z11order_arrayPii")
+    fn.argtypes = [p, i]
+    fn.restype = None
+    fn = getattr(L, "_Z16order_with_trustPii")
+    fn.argtypes = [p, i]
+    fn.restype = None
+    return L
+
+
+lib = _load()
+
+
+def version() -> str:
+    return lib.labsort_version().decode()
+
+
+def _check(status: int, what: str) -> None:
+    if status != OK:
+        msg = lib.labsort_error_string(status).decode()
+        if status == ERR_HIP:
+            msg += ": " + lib.labsort_hip_error_string(lib.labsort_last_hip_error()).decode()
+        raise LabsortError(f"{what} failed: {msg}")
+
+
+def _ptr(x) -> int:
+    """Device or host address of a torch tensor / numpy array / int."""
+    if isinstance(x, int):
+        return x
+    if isinstance(x, np.ndarray):
+        assert x.flags["C_CONTIGUOUS"]
+        return x.ctypes.data
+    assert x.is_contiguous()
+    return x.data_ptr()
+
+
+def _stream(stream) -> int | None:
+    if stream is None:
+        try:
+            import torch
+            if torch.cuda.is_available():
+                return torch.cuda.current_stream().cuda_stream
+        except Exception:
+            pass
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream
+
+
+# ---- host-pointer drop-ins (lab.h) -------------------------------------------------
+def order_array(a: np.ndarray) -> None:
+    """Sort an int32 numpy array in place on the GPU (lab.cu:303 semantics).
+
+    Unlike the C++ drop-in, which prints GPUassert and exits, this raises."""
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    _check(lib.labsort_sort_host(a.ctypes.data, a.size, KEY["i32"], _default_algo()), "order_array")
+
+
+def sort_host(a: np.ndarray, algo: str = "radix") -> None:
+    """Sort a uint32 or int32 numpy array in place through the GPU."""
+    key = "i32" if a.dtype == np.int32 else "u32"
+    assert a.dtype in (np.int32, np.uint32) and a.flags["C_CONTIGUOUS"]
+    _check(lib.labsort_sort_host(a.ctypes.data, a.size, KEY[key], ALGO[algo]), "sort_host")
+
+
+def order_with_trust(a: np.ndarray) -> None:
+    """thrust::sort on the host pointer (lab.cu:404): rocThrust's sequential CPU sort."""
+    assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
+    getattr(lib, "_Z16order_with_trustPii")(a.ctypes.data, a.size)
+
+
+def _default_algo() -> int:
+    return ALGO.get(os.environ.get("LABSORT_ALGO", "radix"), 0)
+
+
+# ---- device API (torch tensors or raw device addresses) ----------------------------
+def workspace_bytes(n: int, algo: str = "radix") -> int:
+    return int(lib.labsort_workspace_bytes(n, ALGO[algo]))
+
+
+def max_keys(algo: str = "radix") -> int:
+    return int(lib.labsort_max_keys(ALGO[algo]))
+
+
+def tile_keys() -> int:
+    return int(lib.labsort_tile_keys())
+
+
+def merge_tile_keys() -> int:
+    return int(lib.labsort_merge_tile_keys())
+
+
+def merge_parts(n: int) -> int:
+    return int(lib.labsort_merge_parts(n))
+
+
+def sort_device(d_in, d_out, n: int, key: str = "u32", algo: str = "radix", workspace=None,
+                workspace_bytes_: int | None = None, stream=None) -> None:
+    """Sort n keys d_in -> d_out (may alias) asynchronously on `stream`."""
+    if workspace is None:
+        import torch
+        workspace = torch.empty(max(workspace_bytes(n, algo), 1), dtype=torch.uint8, device="cuda")
+    wsb = workspace_bytes_ if workspace_bytes_ is not None else (
+        workspace.numel() * workspace.element_size() if hasattr(workspace, "numel") else workspace_bytes(n, algo))
+    _check(lib.labsort_sort_device(_ptr(d_in), _ptr(d_out), n, KEY[key], ALGO[algo], _ptr(workspace), wsb,
+                                   _stream(stream)), "sort_device")
+
+
+def wave_tile_sort(d_keys, n: int, key: str = "u32", stream=None) -> None:
+    _check(lib.labsort_wave_tile_sort(_ptr(d_keys), n, KEY[key], _stream(stream)), "wave_tile_sort")
+
+
+def tile_sort(d_in, d_out, n: int, key: str = "u32", stream=None) -> None:
+    _check(lib.labsort_tile_sort(_ptr(d_in), _ptr(d_out), n, KEY[key], _stream(stream)), "tile_sort")
+
+
+def merge_pass(d_in, d_out, n: int, run: int, d_part, key: str = "u32", stream=None) -> None:
+    _check(lib.labsort_merge_pass(_ptr(d_in), _ptr(d_out), n, run, KEY[key], _ptr(d_part), _stream(stream)),
+           "merge_pass")
+
+
+def merge(d_a, la: int, d_b, lb: int, d_out, d0: int, d1: int, d_part, key: str = "u32", stream=None) -> None:
+    _check(lib.labsort_merge(_ptr(d_a) if la else 0, la, _ptr(d_b) if lb else 0, lb, _ptr(d_out), d0, d1,
+                             KEY[key], _ptr(d_part), _stream(stream)), "merge")
+
+
+def histogram(d_keys, n: int, d_hist, bits: int = 8, key: str = "u32", stream=None) -> None:
+    _check(lib.labsort_histogram(_ptr(d_keys), n, KEY[key], bits, _ptr(d_hist), _stream(stream)), "histogram")
+
+
+def fill(d_out, n: int, seed: int, dist: str = "u32", param: int = 0, first: int = 0, stream=None) -> None:
+    if dist == "reversed" and param == 0:
+        param = first + n
+    _check(lib.labsort_fill(_ptr(d_out), n, seed & (2**64 - 1), DIST[dist], param, first, _stream(stream)),
+           "fill")
+
+
+def count_descents(d_keys, n: int, d_count, key: str = "u32", stream=None) -> None:
+    _check(lib.labsort_count_descents(_ptr(d_keys), n, KEY[key], _ptr(d_count), _stream(stream)),
+           "count_descents")
+
+
+def timing_enable(on: bool = True) -> None:
+    _check(lib.labsort_timing_enable(1 if on else 0), "timing_enable")
+
+
+def timing_read(kclass: str) -> tuple[float, int]:
+    ms, cnt = ctypes.c_double(0.0), ctypes.c_longlong(0)
+    _check(lib.labsort_timing_read(KCLASS[kclass], ctypes.byref(ms), ctypes.byref(cnt)), "timing_read")
+    return ms.value, cnt.value

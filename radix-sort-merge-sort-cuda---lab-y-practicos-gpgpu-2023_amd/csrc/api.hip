@@ -1,0 +1,416 @@
+// api.hip -- host orchestration and the C-ABI of liblabsort.so (include/labsort.h).
+//
+// Replaces the reference's host pipeline `order_array` (lab.cu:303-402):
+//   * device memory is a persistent, grown-on-demand workspace per device instead
+//     of cudaMalloc/cudaFree on every call (lab.cu:313-316, 398-401);
+//   * all stages are queued on one stream with no intermediate device-wide
+//     synchronisation (the reference syncs after each of its 19-21 launches);
+//   * the only host synchronisation is the final D2H copy of the host-pointer API.
+// Error policy of the drop-in order_array: print "GPUassert: ..." and exit(code),
+// as CUDA_CHK/gpuAssert do (utils.h:30-38).  The extern "C" API returns codes.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "../../include/labsort.h"
+#include "common.h"
+
+using namespace labsort;
+
+namespace {
+
+thread_local int g_last_hip = 0;
+
+int fail_hip(hipError_t e) {
+    g_last_hip = (int)e;
+    return LABSORT_ERR_HIP;
+}
+#define HIP_TRY(x)                                   \
+    do {                                             \
+        hipError_t _e = (x);                         \
+        if (_e != hipSuccess) return fail_hip(_e);   \
+    } while (0)
+
+inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+inline uint32_t flip_of(int key_type) { return key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u; }
+inline hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---------------------------------------------------------------------------------
+// timing hooks
+// ---------------------------------------------------------------------------------
+struct TimedLaunch {
+    int cls;
+    hipEvent_t a, b;
+};
+std::mutex g_timing_mu;
+bool g_timing_on = false;
+std::vector<TimedLaunch> g_pending;
+double g_total_ms[LABSORT_K_COUNT];
+long long g_launches[LABSORT_K_COUNT];
+
+struct TimingScope {
+    int cls;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimingScope(int c, hipStream_t st) : cls(c), s(st) {
+        if (!g_timing_on) return;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
+        (void)hipEventRecord(a, s);
+    }
+    ~TimingScope() {
+        if (!a) return;
+        (void)hipEventRecord(b, s);
+        std::lock_guard<std::mutex> lk(g_timing_mu);
+        g_pending.push_back({cls, a, b});
+    }
+};
+
+void timing_collect() {
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    for (auto &t : g_pending) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, t.a, t.b) == hipSuccess) {
+            g_total_ms[t.cls] += ms;
+            g_launches[t.cls] += 1;
+        }
+        (void)hipEventDestroy(t.a);
+        (void)hipEventDestroy(t.b);
+    }
+    g_pending.clear();
+}
+
+// ---------------------------------------------------------------------------------
+// workspace layouts
+// ---------------------------------------------------------------------------------
+struct RadixLayout {
+    int bits, R, P;
+    size_t ntiles;
+    size_t off_tmp, off_hist, off_counter, off_err, off_lookback, zero_bytes, off_plan, total;
+};
+
+RadixLayout radix_layout(size_t n, int bits) {
+    RadixLayout L{};
+    L.bits = bits;
+    L.R = 1 << bits;
+    L.P = (32 + bits - 1) / bits;
+    L.ntiles = (n + OS_TILE - 1) / OS_TILE;
+    size_t o = 0;
+    L.off_tmp = o;
+    o = align_up(o + n * 4, 256);
+    // zeroed block: hist | counters | err | lookback (one memset per sort)
+    L.off_hist = o;
+    o += (size_t)L.P * L.R * 4;
+    L.off_counter = o;
+    o += (size_t)L.P * 4;
+    L.off_err = o;
+    o += 16;
+    o = align_up(o, 256);
+    L.off_lookback = o;
+    o += (size_t)L.P * L.ntiles * L.R * 4;
+    o = align_up(o, 256);
+    L.zero_bytes = o - L.off_hist;
+    L.off_plan = o;
+    o = align_up(o + sizeof(Plan), 256);
+    L.total = o;
+    return L;
+}
+
+struct MergeLayout {
+    size_t off_tmp, off_part, total;
+};
+MergeLayout merge_layout(size_t n) {
+    MergeLayout L{};
+    size_t o = 0;
+    L.off_tmp = o;
+    o = align_up(o + n * 4, 256);
+    L.off_part = o;
+    o = align_up(o + (labsort_merge_parts(n)) * 4, 256);
+    L.total = o;
+    return L;
+}
+
+bool small_path(size_t n, int algo) { return algo != LABSORT_ALGO_RADIX1 && n <= (size_t)TS_TILE; }
+
+int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int bits, char *ws, hipStream_t s) {
+    const RadixLayout L = radix_layout(n, bits);
+    Bufs b;
+    b.p[SEL_IN] = const_cast<uint32_t *>(in);
+    b.p[SEL_OUT] = out;
+    b.p[SEL_TMP] = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
+    uint32_t *hist = reinterpret_cast<uint32_t *>(ws + L.off_hist);
+    uint32_t *counters = reinterpret_cast<uint32_t *>(ws + L.off_counter);
+    uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
+    uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
+    Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
+    HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.zero_bytes, s));
+    {
+        TimingScope ts(LABSORT_K_HISTOGRAM, s);
+        HIP_TRY(launch_histogram(in, n, flip, bits, hist, s));
+    }
+    HIP_TRY(launch_plan(hist, n, bits, in == out ? 1 : 0, plan, s));
+    for (int p = 0; p < L.P; ++p) {
+        TimingScope ts(LABSORT_K_ONESWEEP, s);
+        HIP_TRY(launch_onesweep(b, plan, p, bits, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
+                                counters + p, err, s));
+    }
+    HIP_TRY(launch_final_copy(b, plan, n, s));
+    return LABSORT_OK;
+}
+
+int merge_passes(size_t n) {
+    size_t runs = (n + TS_TILE - 1) / TS_TILE;
+    int m = 0;
+    while (((size_t)1 << m) < runs) ++m;
+    return m;
+}
+
+int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s) {
+    const MergeLayout L = merge_layout(n);
+    uint32_t *tmp = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
+    uint32_t *part = reinterpret_cast<uint32_t *>(ws + L.off_part);
+    const int m = merge_passes(n);
+    uint32_t *cur = (m % 2 == 0) ? out : tmp;
+    {
+        TimingScope ts(LABSORT_K_TILE_SORT, s);
+        HIP_TRY(launch_tile_sort(in, cur, n, flip, s));
+    }
+    size_t run = TS_TILE;
+    for (int k = 0; k < m; ++k) {
+        uint32_t *nxt = (cur == out) ? tmp : out;
+        TimingScope ts(LABSORT_K_MERGE, s);
+        HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s));
+        cur = nxt;
+        run *= 2;
+    }
+    return LABSORT_OK;
+}
+
+// ---------------------------------------------------------------------------------
+// host-pointer API state: one cached device buffer + workspace per device
+// ---------------------------------------------------------------------------------
+struct DeviceCache {
+    void *keys = nullptr;
+    size_t keys_bytes = 0;
+    void *ws = nullptr;
+    size_t ws_bytes = 0;
+    hipStream_t stream = nullptr;
+};
+std::mutex g_host_mu;
+std::vector<DeviceCache> g_cache;
+
+int ensure_buffer(void **p, size_t *have, size_t need) {
+    if (*have >= need && *p) return LABSORT_OK;
+    if (*p) {
+        HIP_TRY(hipFree(*p));
+        *p = nullptr;
+        *have = 0;
+    }
+    size_t want = need < (1u << 20) ? (1u << 20) : need;
+    HIP_TRY(hipMalloc(p, want));
+    *have = want;
+    return LABSORT_OK;
+}
+
+int default_algo() {
+    const char *e = std::getenv("LABSORT_ALGO");
+    if (!e) return LABSORT_ALGO_RADIX;
+    if (!std::strcmp(e, "merge")) return LABSORT_ALGO_MERGE;
+    if (!std::strcmp(e, "radix1")) return LABSORT_ALGO_RADIX1;
+    return LABSORT_ALGO_RADIX;
+}
+
+}  // namespace
+
+// =================================================================================
+// C-ABI
+// =================================================================================
+extern "C" {
+
+const char *labsort_version(void) { return "labsort 0.1 (gfx950)"; }
+
+const char *labsort_error_string(int status) {
+    switch (status) {
+    case LABSORT_OK: return "ok";
+    case LABSORT_ERR_ARG: return "invalid argument";
+    case LABSORT_ERR_HIP: return "HIP runtime error";
+    case LABSORT_ERR_DEVICE: return "device-side error (look-back spin limit)";
+    default: return "unknown status";
+    }
+}
+
+int labsort_last_hip_error(void) { return g_last_hip; }
+const char *labsort_hip_error_string(int e) { return hipGetErrorString((hipError_t)e); }
+
+size_t labsort_max_keys(int algo) {
+    if (algo == LABSORT_ALGO_MERGE) return (size_t)0x7FFFFFFFu;
+    return RADIX_MAX_N;
+}
+size_t labsort_tile_keys(void) { return (size_t)TS_TILE; }
+size_t labsort_merge_tile_keys(void) { return (size_t)MG_TILE; }
+size_t labsort_merge_parts(size_t n) { return (n + MG_TILE - 1) / MG_TILE + 2; }
+
+size_t labsort_workspace_bytes(size_t n, int algo) {
+    if (small_path(n, algo)) return 256;
+    switch (algo) {
+    case LABSORT_ALGO_RADIX: return radix_layout(n, 8).total;
+    case LABSORT_ALGO_RADIX1: return radix_layout(n, 1).total;
+    case LABSORT_ALGO_MERGE: return merge_layout(n).total;
+    default: return 0;
+    }
+}
+
+int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, int algo, void *d_ws,
+                        size_t ws_bytes, void *stream) {
+    if (n == 0) return LABSORT_OK;
+    if (!d_in || !d_out) return LABSORT_ERR_ARG;
+    if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
+    if (algo != LABSORT_ALGO_RADIX && algo != LABSORT_ALGO_MERGE && algo != LABSORT_ALGO_RADIX1)
+        return LABSORT_ERR_ARG;
+    if (n > labsort_max_keys(algo)) return LABSORT_ERR_ARG;
+    if (ws_bytes < labsort_workspace_bytes(n, algo) || !d_ws) return LABSORT_ERR_ARG;
+    const uint32_t flip = flip_of(key_type);
+    hipStream_t s = as_stream(stream);
+    const uint32_t *in = static_cast<const uint32_t *>(d_in);
+    uint32_t *out = static_cast<uint32_t *>(d_out);
+    if (small_path(n, algo)) {
+        TimingScope ts(LABSORT_K_TILE_SORT, s);
+        HIP_TRY(launch_tile_sort(in, out, n, flip, s));
+        return LABSORT_OK;
+    }
+    char *ws = static_cast<char *>(d_ws);
+    if (algo == LABSORT_ALGO_MERGE) return sort_merge(in, out, n, flip, ws, s);
+    return sort_radix(in, out, n, flip, algo == LABSORT_ALGO_RADIX1 ? 1 : 8, ws, s);
+}
+
+int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo) {
+    if (n == 0) return LABSORT_OK;
+    if (!h_keys) return LABSORT_ERR_ARG;
+    if (n > labsort_max_keys(algo)) return LABSORT_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    if ((int)g_cache.size() <= dev) g_cache.resize(dev + 1);
+    DeviceCache &c = g_cache[dev];
+    if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    int st = ensure_buffer(&c.keys, &c.keys_bytes, n * 4);
+    if (st) return st;
+    const size_t wsb = labsort_workspace_bytes(n, algo);
+    st = ensure_buffer(&c.ws, &c.ws_bytes, wsb);
+    if (st) return st;
+    HIP_TRY(hipMemcpyAsync(c.keys, h_keys, n * 4, hipMemcpyHostToDevice, c.stream));
+    st = labsort_sort_device(c.keys, c.keys, n, key_type, algo, c.ws, c.ws_bytes, c.stream);
+    if (st) return st;
+    HIP_TRY(hipMemcpyAsync(h_keys, c.keys, n * 4, hipMemcpyDeviceToHost, c.stream));
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    if (!small_path(n, algo) && algo != LABSORT_ALGO_MERGE) {
+        const RadixLayout L = radix_layout(n, algo == LABSORT_ALGO_RADIX1 ? 1 : 8);
+        uint32_t err = 0;
+        HIP_TRY(hipMemcpy(&err, static_cast<char *>(c.ws) + L.off_err, 4, hipMemcpyDeviceToHost));
+        if (err) return LABSORT_ERR_DEVICE;
+    }
+    return LABSORT_OK;
+}
+
+int labsort_wave_tile_sort(void *d_keys, size_t n, int key_type, void *stream) {
+    if (n == 0) return LABSORT_OK;
+    if (!d_keys || n > 0xFFFFFFC0u) return LABSORT_ERR_ARG;
+    HIP_TRY(launch_wave_tile_sort(static_cast<uint32_t *>(d_keys), n, flip_of(key_type), as_stream(stream)));
+    return LABSORT_OK;
+}
+
+int labsort_tile_sort(const void *d_in, void *d_out, size_t n, int key_type, void *stream) {
+    if (n == 0) return LABSORT_OK;
+    if (!d_in || !d_out || n > 0x7FFFFFFFu) return LABSORT_ERR_ARG;
+    TimingScope ts(LABSORT_K_TILE_SORT, as_stream(stream));
+    HIP_TRY(launch_tile_sort(static_cast<const uint32_t *>(d_in), static_cast<uint32_t *>(d_out), n,
+                             flip_of(key_type), as_stream(stream)));
+    return LABSORT_OK;
+}
+
+int labsort_merge_pass(const void *d_in, void *d_out, size_t n, size_t run, int key_type, uint32_t *d_part,
+                       void *stream) {
+    if (n == 0) return LABSORT_OK;
+    if (!d_in || !d_out || !d_part || d_in == d_out || n > 0x7FFFFFFFu) return LABSORT_ERR_ARG;
+    if (run == 0 || (run & (run - 1)) != 0 || 2 * run < (size_t)MG_TILE) return LABSORT_ERR_ARG;
+    TimingScope ts(LABSORT_K_MERGE, as_stream(stream));
+    HIP_TRY(launch_merge_pass(static_cast<const uint32_t *>(d_in), static_cast<uint32_t *>(d_out), n, run,
+                              flip_of(key_type), d_part, as_stream(stream)));
+    return LABSORT_OK;
+}
+
+int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *d_out, size_t d0, size_t d1,
+                  int key_type, uint32_t *d_part, void *stream) {
+    if (d1 < d0 || d1 > la + lb || la + lb > 0x7FFFFFFFu) return LABSORT_ERR_ARG;
+    if (d1 == d0) return LABSORT_OK;
+    if (!d_out || !d_part || (la && !d_a) || (lb && !d_b)) return LABSORT_ERR_ARG;
+    TimingScope ts(LABSORT_K_MERGE, as_stream(stream));
+    HIP_TRY(launch_merge_ab(static_cast<const uint32_t *>(d_a), la, static_cast<const uint32_t *>(d_b), lb,
+                            static_cast<uint32_t *>(d_out), d0, d1, flip_of(key_type), d_part, as_stream(stream)));
+    return LABSORT_OK;
+}
+
+int labsort_histogram(const void *d_keys, size_t n, int key_type, int bits, uint32_t *d_hist, void *stream) {
+    if (n == 0) return LABSORT_OK;
+    if (!d_keys || !d_hist || (bits != 8 && bits != 1)) return LABSORT_ERR_ARG;
+    TimingScope ts(LABSORT_K_HISTOGRAM, as_stream(stream));
+    HIP_TRY(launch_histogram(static_cast<const uint32_t *>(d_keys), n, flip_of(key_type), bits, d_hist,
+                             as_stream(stream)));
+    return LABSORT_OK;
+}
+
+int labsort_fill(void *d_out, size_t n, uint64_t seed, int dist, uint64_t param, uint64_t first, void *stream) {
+    if (n == 0) return LABSORT_OK;
+    if (!d_out || dist < 0 || dist > 7) return LABSORT_ERR_ARG;
+    HIP_TRY(launch_fill(static_cast<uint32_t *>(d_out), n, seed, dist, param, first, as_stream(stream)));
+    return LABSORT_OK;
+}
+
+int labsort_count_descents(const void *d_keys, size_t n, int key_type, uint32_t *d_count, void *stream) {
+    if (n < 2) return LABSORT_OK;
+    if (!d_keys || !d_count) return LABSORT_ERR_ARG;
+    HIP_TRY(launch_count_descents(static_cast<const uint32_t *>(d_keys), n, flip_of(key_type), d_count,
+                                  as_stream(stream)));
+    return LABSORT_OK;
+}
+
+int labsort_timing_enable(int on) {
+    timing_collect();
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    g_timing_on = on != 0;
+    for (int i = 0; i < LABSORT_K_COUNT; ++i) {
+        g_total_ms[i] = 0.0;
+        g_launches[i] = 0;
+    }
+    return LABSORT_OK;
+}
+
+int labsort_timing_read(int cls, double *total_ms, long long *launches) {
+    if (cls < 0 || cls >= LABSORT_K_COUNT || !total_ms || !launches) return LABSORT_ERR_ARG;
+    timing_collect();
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    *total_ms = g_total_ms[cls];
+    *launches = g_launches[cls];
+    return LABSORT_OK;
+}
+
+void sort(int *in, int n) {
+    if (n <= 0) return;
+    const int st = labsort_sort_host(in, (size_t)n, LABSORT_KEY_I32, default_algo());
+    if (st != LABSORT_OK) {
+        std::fprintf(stderr, "GPUassert: %s %s %d\n",
+                     st == LABSORT_ERR_HIP ? hipGetErrorString((hipError_t)g_last_hip) : labsort_error_string(st),
+                     __FILE__, __LINE__);
+        std::exit(st == LABSORT_ERR_HIP ? g_last_hip : 1);
+    }
+}
+
+}  // extern "C"
+
+// =================================================================================
+// C++-linkage drop-ins (lab.h:9-10): same mangled names as the reference build.
+// =================================================================================
+void order_array(int *srcCpu, int length) { sort(srcCpu, length); }

@@ -1,0 +1,71 @@
+// common.h -- shared definitions of the labsort HIP kernels and host launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace labsort {
+
+constexpr int WAVE = 64;
+
+// ---- radix configuration (8-bit digits, onesweep) ----
+constexpr int RADIX_BITS = 8;
+constexpr int OS_BLOCK = 512;     // threads per onesweep workgroup (8 waves)
+constexpr int OS_KPT = 16;        // keys per thread
+constexpr int OS_TILE = OS_BLOCK * OS_KPT;  // 8192 keys per tile
+constexpr int HIST_BLOCK = 1024;
+
+// ---- LDS tile sort (merge path stage 1 / small sorts) ----
+constexpr int TS_BLOCK = 512;
+constexpr int TS_KPT = 16;
+constexpr int TS_TILE = TS_BLOCK * TS_KPT;  // 8192-key sorted runs
+
+// ---- merge path ----
+constexpr int MG_BLOCK = 256;
+constexpr int MG_KPT = 16;
+constexpr int MG_TILE = MG_BLOCK * MG_KPT;  // 4096 outputs per workgroup
+
+constexpr int MAX_PASSES = 32;
+constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_SKIP = 0xFFu;
+
+// Per-sort plan written on the device after the histogram (no host sync):
+// which buffer each digit pass reads and writes, or SKIP when every key has
+// the same digit in that pass (the deterministic counterpart of the
+// reference's "stop when sorted" test, lab.cu:61).
+struct Plan {
+    uint32_t src[MAX_PASSES];
+    uint32_t dst[MAX_PASSES];
+    uint32_t copy_from;  // SEL_SKIP: result already in OUT
+    uint32_t active;     // number of non-trivial passes
+    uint32_t pad[2];
+};
+
+struct Bufs {
+    uint32_t *p[3];  // IN, OUT, TMP
+};
+
+// lookback word: 2 status bits + 30-bit count (n < 2^30 per radix sort)
+constexpr uint32_t LB_AGG = 1u << 30;
+constexpr uint32_t LB_INC = 2u << 30;
+constexpr uint32_t LB_VAL = (1u << 30) - 1u;
+constexpr size_t RADIX_MAX_N = (size_t)LB_VAL;  // 2^30 - 1
+
+// ---- host launchers (kernels.hip) ----
+hipError_t launch_fill(uint32_t *out, size_t n, uint64_t seed, int dist, uint64_t param, uint64_t first,
+                       hipStream_t s);
+hipError_t launch_histogram(const uint32_t *keys, size_t n, uint32_t flip, int bits, uint32_t *hist,
+                            hipStream_t s);
+hipError_t launch_plan(const uint32_t *hist, size_t n, int bits, int in_is_out, Plan *plan, hipStream_t s);
+hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t n, uint32_t flip,
+                           const uint32_t *hist, uint32_t *lookback, uint32_t *counter, uint32_t *err,
+                           hipStream_t s);
+hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
+hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
+hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);
+hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t run, uint32_t flip,
+                             uint32_t *part, hipStream_t s);
+hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size_t lb, uint32_t *out, size_t d0,
+                           size_t d1, uint32_t flip, uint32_t *part, hipStream_t s);
+hipError_t launch_count_descents(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *count, hipStream_t s);
+
+}  // namespace labsort

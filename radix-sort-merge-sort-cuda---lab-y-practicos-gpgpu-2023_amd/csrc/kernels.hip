@@ -1,0 +1,721 @@
+// kernels.hip -- hand-written HIP kernels of the labsort path for gfx950 (CDNA4).
+//
+// Everything here is 32-bit integer / permute work: no MFMA.  Keys are plain
+// 32-bit words; signed (int) order is obtained by XOR-ing the sign bit into
+// every digit extraction and comparison (`flip`), so one code path serves the
+// reference's int keys (lab.h:9) and the north_star's uint32 keys.
+//
+// Kernel map (reference counterpart in `Sord Radix y Merge/lab.cu`):
+//   k_wave_split      radix_sort_kernel :47-87 + exlusiveScan :11-41 -- a 64-key
+//                     tile per wave, 1-bit split per iteration with ballot/mbcnt
+//                     (the split's scan) and ds_permute (the scatter), early exit
+//                     when the tile is sorted (:61).
+//   k_histogram       letra.pdf's global "totalFalses" generalised to 8-bit digits,
+//                     all passes in one read of the keys.
+//   k_onesweep        one LSD pass: block-local rank (wave64 match + per-wave
+//                     counters), decoupled look-back for the global exclusive
+//                     offsets, LDS reorder, coalesced scatter.
+//   k_tile_sort       stage 1+2 of order_array (lab.cu:323-346): an LDS-resident
+//                     8192-key LSD radix sort per workgroup.
+//   k_merge_*         stage 3 (separators_kernel :209-270 + merge_segments_kernel
+//                     :272-300) as merge-path: a co-rank search per output tile
+//                     (busquedaPorBiparticion :102-132, same tie rule: A before B
+//                     on equal keys) and an LDS merge per tile.
+#include "common.h"
+
+namespace labsort {
+
+// ---------------------------------------------------------------------------------
+// small device helpers
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t ld_agent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Lanes whose digit equals mine (all 64 lanes active): BITS ballots.
+template <int BITS>
+__device__ __forceinline__ uint64_t match_digit(uint32_t d) {
+    uint64_t m = ~0ull;
+#pragma unroll
+    for (int b = 0; b < BITS; ++b) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t bal = __ballot(bit);
+        m &= bit ? bal : ~bal;
+    }
+    return m;
+}
+
+// Exclusive scan over the first R threads of the block (value v in thread tid < R,
+// others pass 0).  Must be called by every thread (contains a barrier when R > 64).
+template <int BLOCK, int R>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *wsum) {
+    const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = __shfl_up(x, off);
+        if (lane >= (uint32_t)off) x += t;
+    }
+    if constexpr (R > 64) {
+        constexpr int NW = R / 64;
+        if (lane == 63 && wid < (uint32_t)NW) wsum[wid] = x;
+        __syncthreads();
+        uint32_t add = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+            if ((uint32_t)w < wid) add += wsum[w];
+        x += add;
+    }
+    return x - v;
+}
+
+// Stable rank of KPT digits per lane inside one wave (slot-major order: slot j of
+// lane l is element j*64+l of the wave's stripe).  `wh` = this wave's R counters
+// (zeroed); on return wh[d] = count of digit d in the wave.
+template <int BITS, int KPT>
+__device__ __forceinline__ void wave_rank(const uint32_t (&dig)[KPT], uint32_t (&rank)[KPT], uint32_t *wh) {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t d = dig[j];
+        const uint64_t m = match_digit<BITS>(d);
+        const uint32_t pre = mbcnt64(m);
+        const uint32_t old = wh[d];  // peers read the same word (broadcast)
+        if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);  // one leader per digit
+        rank[j] = old + pre;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// generator (same formula as oracle/cpu_sort.cpp)
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void k_fill(uint32_t *__restrict__ out, size_t n, uint64_t seed, int dist,
+                                              uint64_t param, uint64_t first) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t gi = first + i;
+        const uint64_t z = mix64(seed ^ (gi * 0x9E3779B97F4A7C15ull));
+        const uint32_t hi = (uint32_t)(z >> 32);
+        uint32_t v;
+        switch (dist) {
+        case 1: v = (uint32_t)(z >> 33); break;
+        case 2: v = hi % 100u; break;
+        case 3: v = hi % 1000u; break;
+        case 4: v = (uint32_t)gi; break;
+        case 5: v = (uint32_t)(param - 1 - gi); break;
+        case 6: v = (uint32_t)param; break;
+        case 7: v = param >= 32 ? hi : (hi & (uint32_t)((1ull << param) - 1)); break;
+        default: v = hi; break;
+        }
+        out[i] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// upfront histogram of every digit pass (one read of the keys)
+// LDS counters laid out [pass][digit][32 slots], slot = lane & 31, so the 32 lanes
+// of a ds_add group always hit 32 different banks (conflict-free for any data).
+// ---------------------------------------------------------------------------------
+template <int BITS>
+__global__ __launch_bounds__(HIST_BLOCK) void k_histogram(const uint32_t *__restrict__ keys, size_t n, uint32_t flip,
+                                                          uint32_t *__restrict__ hist) {
+    constexpr int R = 1 << BITS, P = (32 + BITS - 1) / BITS, SLOTS = 32;
+    constexpr uint32_t RM = R - 1;
+    __shared__ uint32_t h[P * R * SLOTS];
+    for (int i = threadIdx.x; i < P * R * SLOTS; i += HIST_BLOCK) h[i] = 0u;
+    __syncthreads();
+    const uint32_t slot = threadIdx.x & 31u;
+    auto count = [&](uint32_t k) {
+        k ^= flip;
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+            const uint32_t d = (k >> (p * BITS)) & RM;
+            atomicAdd(&h[(p * R + d) * SLOTS + slot], 1u);
+        }
+    };
+    // contiguous chunk per workgroup, multiple of 64 keys
+    const size_t per = (((n + gridDim.x - 1) / gridDim.x) + 63) & ~(size_t)63;
+    const size_t beg = (size_t)blockIdx.x * per;
+    const size_t end = beg + per < n ? beg + per : n;
+    if (beg < end) {
+        if ((((uintptr_t)(keys + beg)) & 15u) == 0) {
+            const uint4 *v = reinterpret_cast<const uint4 *>(keys + beg);
+            const size_t nv = (end - beg) / 4;
+            size_t i = threadIdx.x;
+            for (; i + 3 * HIST_BLOCK < nv; i += 4 * HIST_BLOCK) {
+                uint4 x[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) x[u] = v[i + u * HIST_BLOCK];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    count(x[u].x); count(x[u].y); count(x[u].z); count(x[u].w);
+                }
+            }
+            for (; i < nv; i += HIST_BLOCK) {
+                const uint4 x = v[i];
+                count(x.x); count(x.y); count(x.z); count(x.w);
+            }
+            for (size_t t = beg + nv * 4 + threadIdx.x; t < end; t += HIST_BLOCK) count(keys[t]);
+        } else {
+            for (size_t t = beg + threadIdx.x; t < end; t += HIST_BLOCK) count(keys[t]);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < P * R; i += HIST_BLOCK) {
+        uint32_t s = 0;
+#pragma unroll 8
+        for (int q = 0; q < SLOTS; ++q) s += h[i * SLOTS + ((q + i) & (SLOTS - 1))];
+        if (s) atomicAdd(&hist[i], s);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// pass plan: skip passes whose digit is the same for every key; choose buffers so
+// the last non-trivial pass writes OUT and no pass scatters in place.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_plan(const uint32_t *__restrict__ hist, uint32_t n, int bits,
+                                              int in_is_out, Plan *__restrict__ plan) {
+    __shared__ uint32_t triv[MAX_PASSES];
+    const int R = 1 << bits, P = (32 + bits - 1) / bits;
+    if (threadIdx.x < MAX_PASSES) triv[threadIdx.x] = 0;
+    __syncthreads();
+    for (int p = 0; p < P; ++p)
+        for (int d = threadIdx.x; d < R; d += blockDim.x)
+            if (hist[p * R + d] == n) triv[p] = 1;
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    int act[MAX_PASSES];
+    int k = 0;
+    for (int p = 0; p < MAX_PASSES; ++p) {
+        plan->src[p] = SEL_SKIP;
+        plan->dst[p] = SEL_SKIP;
+        if (p < P && !triv[p]) act[k++] = p;
+    }
+    plan->active = (uint32_t)k;
+    if (k == 0) {
+        plan->copy_from = in_is_out ? SEL_SKIP : SEL_IN;
+        return;
+    }
+    uint32_t d[MAX_PASSES];
+    uint32_t cur = SEL_OUT;
+    for (int i = k - 1; i >= 0; --i) {
+        d[i] = cur;
+        cur = (cur == SEL_OUT) ? SEL_TMP : SEL_OUT;
+    }
+    if (in_is_out && d[0] == SEL_OUT)  // first pass would read and write the same buffer
+        for (int i = 0; i < k; ++i) d[i] = (i & 1) ? SEL_OUT : SEL_TMP;
+    uint32_t src = SEL_IN;
+    for (int i = 0; i < k; ++i) {
+        plan->src[act[i]] = src;
+        plan->dst[act[i]] = d[i];
+        src = d[i];
+    }
+    plan->copy_from = (d[k - 1] == SEL_OUT) ? SEL_SKIP : d[k - 1];
+}
+
+__global__ __launch_bounds__(256) void k_final_copy(Bufs b, const Plan *__restrict__ plan, size_t n) {
+    const uint32_t from = plan->copy_from;
+    if (from == SEL_SKIP) return;
+    const uint32_t *__restrict__ src = b.p[from];
+    uint32_t *__restrict__ dst = b.p[SEL_OUT];
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
+        const size_t nv = n / 4;
+        for (size_t i = tid; i < nv; i += stride)
+            reinterpret_cast<uint4 *>(dst)[i] = reinterpret_cast<const uint4 *>(src)[i];
+        for (size_t i = nv * 4 + tid; i < n; i += stride) dst[i] = src[i];
+    } else {
+        for (size_t i = tid; i < n; i += stride) dst[i] = src[i];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// one LSD radix pass ("onesweep"): rank, look-back, LDS reorder, coalesced scatter
+// ---------------------------------------------------------------------------------
+template <int BITS, int BLOCK, int KPT>
+struct OsSmem {
+    static constexpr int R = 1 << BITS, W = BLOCK / WAVE, TILE = BLOCK * KPT;
+    uint32_t keys[TILE];
+    uint32_t whist[W * R];
+    uint32_t gscan[R];
+    uint32_t dstart[R];
+    uint32_t delta[R];
+    uint32_t wsum0[W];
+    uint32_t wsum1[W];
+    uint32_t tile;
+};
+
+constexpr uint32_t SPIN_LIMIT = 1u << 22;
+
+template <int BITS, int BLOCK, int KPT>
+__global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n,
+                                                    uint32_t flip, const uint32_t *__restrict__ ghist,
+                                                    uint32_t *lookback, uint32_t *counter, uint32_t *err) {
+    using S = OsSmem<BITS, BLOCK, KPT>;
+    constexpr int R = S::R, W = S::W, TILE = S::TILE;
+    constexpr uint32_t RM = R - 1;
+    static_assert(R <= BLOCK, "one thread per digit");
+    __shared__ S sm;
+
+    const uint32_t srcsel = plan->src[pass];
+    if (srcsel == SEL_SKIP) return;  // every key has the same digit: identity pass
+    const uint32_t *__restrict__ in = bufs.p[srcsel];
+    uint32_t *__restrict__ out = bufs.p[plan->dst[pass]];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t shift = (uint32_t)pass * BITS;
+
+    if (tid == 0) sm.tile = atomicAdd(counter, 1u);  // dynamic tile id: predecessors already run
+    for (uint32_t i = tid; i < (uint32_t)(W * R); i += BLOCK) sm.whist[i] = 0u;
+    const uint32_t gcount = tid < (uint32_t)R ? ghist[pass * R + tid] : 0u;
+    const uint32_t gex = block_excl_scan<BLOCK, R>(gcount, sm.wsum0);
+    if (tid < (uint32_t)R) sm.gscan[tid] = gex;
+    __syncthreads();
+
+    const uint32_t tile = sm.tile;
+    const uint32_t base = tile * (uint32_t)TILE;
+    const uint32_t nvalid = (n - base) < (uint32_t)TILE ? (n - base) : (uint32_t)TILE;
+    const uint32_t sentinel = ~flip;  // digit RM in every pass: ranks after all real keys
+
+    uint32_t k[KPT];
+    const uint32_t wbase = base + wid * (KPT * WAVE) + lane;
+    if (nvalid == (uint32_t)TILE) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = in[wbase + j * WAVE];
+    } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            k[j] = idx < n ? in[idx] : sentinel;
+        }
+    }
+    uint32_t dig[KPT], rank[KPT];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) dig[j] = ((k[j] ^ flip) >> shift) & RM;
+    uint32_t *wh = sm.whist + wid * R;
+    wave_rank<BITS, KPT>(dig, rank, wh);
+    __syncthreads();
+
+    // per digit: exclusive prefix over waves, tile total
+    uint32_t tot = 0;
+    if (tid < (uint32_t)R) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint32_t c = sm.whist[w * R + tid];
+            sm.whist[w * R + tid] = tot;
+            tot += c;
+        }
+    }
+    const uint32_t agg = (tid == RM) ? tot - ((uint32_t)TILE - nvalid) : tot;  // drop sentinels
+    uint32_t *lb_mine = lookback + (size_t)tile * R + tid;
+    if (tid < (uint32_t)R) st_agent(lb_mine, (tile == 0 ? LB_INC : LB_AGG) | agg);  // publish early
+    const uint32_t dstart = block_excl_scan<BLOCK, R>(tot, sm.wsum1);
+    if (tid < (uint32_t)R) sm.dstart[tid] = dstart;
+    __syncthreads();
+
+    // reorder the tile by digit in LDS
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) sm.keys[sm.dstart[dig[j]] + wh[dig[j]] + rank[j]] = k[j];
+
+    // decoupled look-back: exclusive count of my digit in all earlier tiles
+    if (tid < (uint32_t)R) {
+        uint32_t excl = 0;
+        if (tile > 0) {
+            uint32_t t = tile - 1, spins = 0;
+            for (;;) {
+                const uint32_t w = ld_agent(lookback + (size_t)t * R + tid);
+                if ((w & ~LB_VAL) == 0u) {
+                    if (++spins > SPIN_LIMIT) {
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += w & LB_VAL;
+                if (w & LB_INC) break;
+                --t;
+            }
+            st_agent(lb_mine, LB_INC | (excl + agg));
+        }
+        sm.delta[tid] = sm.gscan[tid] + excl - dstart;
+    }
+    __syncthreads();
+
+    // coalesced scatter: consecutive threads write consecutive slots of a digit run
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t i = (uint32_t)j * BLOCK + tid;
+        if (i < nvalid) {
+            const uint32_t key = sm.keys[i];
+            const uint32_t d = ((key ^ flip) >> shift) & RM;
+            out[sm.delta[d] + i] = key;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// LDS-resident tile sort: 8-bit LSD passes entirely in LDS, one global read and write
+// ---------------------------------------------------------------------------------
+template <int BLOCK, int KPT>
+struct TsSmem {
+    static constexpr int R = 256, W = BLOCK / WAVE, TILE = BLOCK * KPT;
+    uint32_t keys[TILE];
+    uint32_t whist[W * R];
+    uint32_t dstart[R];
+    uint32_t wsum[W];
+    uint32_t red_and[W];
+    uint32_t red_or[W];
+};
+
+template <int BLOCK, int KPT>
+__global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t flip) {
+    using S = TsSmem<BLOCK, KPT>;
+    constexpr int R = S::R, W = S::W, TILE = S::TILE;
+    __shared__ S sm;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t base = blockIdx.x * (uint32_t)TILE;
+    const uint32_t sentinel = ~flip;
+    const uint32_t wbase = base + wid * (KPT * WAVE) + lane;
+
+    uint32_t k[KPT];
+    uint32_t a = ~0u, o = 0u;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t idx = wbase + j * WAVE;
+        const bool ok = idx < n;
+        k[j] = ok ? in[idx] : sentinel;
+        const uint32_t x = k[j] ^ flip;
+        a &= ok ? x : ~0u;
+        o |= ok ? x : 0u;
+    }
+    // bits on which the tile's keys differ -> passes that are not the identity
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a &= __shfl_xor(a, off);
+        o |= __shfl_xor(o, off);
+    }
+    if (lane == 0) {
+        sm.red_and[wid] = a;
+        sm.red_or[wid] = o;
+    }
+    __syncthreads();
+    uint32_t diff = 0;
+    {
+        uint32_t aa = ~0u, oo = 0u;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            aa &= sm.red_and[w];
+            oo |= sm.red_or[w];
+        }
+        diff = aa ^ oo;
+    }
+    uint32_t *wh = sm.whist + wid * R;
+    for (int pass = 0; pass < 4; ++pass) {
+        const uint32_t shift = pass * 8;
+        if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the block
+        for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
+        uint32_t dig[KPT], rank[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) dig[j] = ((k[j] ^ flip) >> shift) & 0xFFu;
+        wave_rank<8, KPT>(dig, rank, wh);
+        __syncthreads();
+        uint32_t tot = 0;
+        if (tid < (uint32_t)R) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t c = sm.whist[w * R + tid];
+                sm.whist[w * R + tid] = tot;
+                tot += c;
+            }
+        }
+        const uint32_t ds = block_excl_scan<BLOCK, R>(tot, sm.wsum);
+        if (tid < (uint32_t)R) sm.dstart[tid] = ds;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) sm.keys[sm.dstart[dig[j]] + wh[dig[j]] + rank[j]] = k[j];
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
+    }
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t idx = wbase + j * WAVE;
+        if (idx < n) out[idx] = k[j];
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// 64-key tile bit-split sort (radix_sort_kernel's job on a wave64)
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_wave_split(uint32_t *keys, uint32_t n, uint32_t flip) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t gw = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t idx = gw * 64u + lane;
+    if (gw * 64u >= n) return;  // wave-uniform
+    uint32_t v = idx < n ? (keys[idx] ^ flip) : 0xFFFFFFFFu;
+    for (int b = 0; b < 32; ++b) {
+        const uint32_t prev = __shfl_up(v, 1);
+        if (__all(lane == 0 || prev <= v)) break;  // tile sorted: stop (lab.cu:61)
+        const bool zero = ((v >> b) & 1u) == 0u;
+        const uint64_t bal = __ballot(zero);        // the split's flags
+        const uint32_t below = mbcnt64(bal);          // exclusive scan of the flags
+        const uint32_t nz = (uint32_t)__popcll(bal);  // totalFalses
+        const uint32_t pos = zero ? below : nz + (lane - below);
+        v = (uint32_t)__builtin_amdgcn_ds_permute((int)(pos << 2), (int)v);  // scatter
+    }
+    if (idx < n) keys[idx] = v ^ flip;
+}
+
+// ---------------------------------------------------------------------------------
+// merge path
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ bool key_le(uint32_t a, uint32_t b, uint32_t flip) { return (a ^ flip) <= (b ^ flip); }
+
+// number of A elements among the first `diag` of merge(A,B), A first on ties
+__device__ __forceinline__ uint32_t corank(const uint32_t *A, uint32_t la, const uint32_t *B, uint32_t lb,
+                                           uint32_t diag, uint32_t flip) {
+    uint32_t lo = diag > lb ? diag - lb : 0u;
+    uint32_t hi = diag < la ? diag : la;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (key_le(A[mid], B[diag - 1u - mid], flip)) lo = mid + 1u;
+        else hi = mid;
+    }
+    return lo;
+}
+
+struct MgSmem {
+    uint32_t in[MG_TILE];
+    uint32_t out[MG_TILE + MG_TILE / 32];
+};
+
+// merge A[a0,a1) and B[b0,b1) (a1-a0 + b1-b0 <= MG_TILE) into out[0 ..)
+template <int BLOCK, int KPT>
+__device__ __forceinline__ void merge_tile(const uint32_t *__restrict__ A, uint32_t a0, uint32_t a1,
+                                           const uint32_t *__restrict__ B, uint32_t b0, uint32_t b1,
+                                           uint32_t *__restrict__ out, uint32_t flip, MgSmem &sm) {
+    const uint32_t tid = threadIdx.x;
+    const uint32_t la = a1 - a0, lb = b1 - b0, tot = la + lb;
+    for (uint32_t i = tid; i < la; i += BLOCK) sm.in[i] = A[a0 + i];
+    for (uint32_t i = tid; i < lb; i += BLOCK) sm.in[la + i] = B[b0 + i];
+    __syncthreads();
+    const uint32_t *sa = sm.in, *sb = sm.in + la;
+    const uint32_t d = tid * KPT < tot ? tid * KPT : tot;
+    uint32_t ai = corank(sa, la, sb, lb, d, flip);
+    uint32_t bi = d - ai;
+    uint32_t va = ai < la ? sa[ai] : 0u;
+    uint32_t vb = bi < lb ? sb[bi] : 0u;
+    uint32_t r[KPT];
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const bool takeA = (bi >= lb) || (ai < la && key_le(va, vb, flip));
+        r[j] = takeA ? va : vb;
+        if (takeA) {
+            ++ai;
+            va = ai < la ? sa[ai] : 0u;
+        } else {
+            ++bi;
+            vb = bi < lb ? sb[bi] : 0u;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t idx = tid * KPT + j;
+        if (idx < tot) sm.out[idx + (idx >> 5)] = r[j];
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < tot; i += BLOCK) out[i] = sm.out[i + (i >> 5)];
+}
+
+struct PairGeom {
+    uint32_t pb, la, lb;
+};
+__device__ __forceinline__ PairGeom pair_of(uint32_t o, uint32_t n, uint32_t run) {
+    PairGeom g;
+    g.pb = (o / (2u * run)) * (2u * run);
+    const uint32_t rest = n - g.pb;
+    g.la = rest < run ? rest : run;
+    const uint32_t restb = rest - g.la;
+    g.lb = restb < run ? restb : run;
+    return g;
+}
+
+// co-rank at the start of every output tile of a merge pass
+__global__ __launch_bounds__(256) void k_merge_part_pass(const uint32_t *__restrict__ src, uint32_t n, uint32_t run,
+                                                         uint32_t flip, uint32_t *__restrict__ part,
+                                                         uint32_t ntiles) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntiles) return;
+    const uint32_t o = i * (uint32_t)MG_TILE;
+    const PairGeom g = pair_of(o, n, run);
+    part[i] = corank(src + g.pb, g.la, src + g.pb + g.la, g.lb, o - g.pb, flip);
+}
+
+template <int BLOCK, int KPT>
+__global__ __launch_bounds__(BLOCK) void k_merge_pass(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                                      uint32_t n, uint32_t run, uint32_t flip,
+                                                      const uint32_t *__restrict__ part) {
+    __shared__ MgSmem sm;
+    const uint32_t i = blockIdx.x;
+    const uint32_t o0 = i * (uint32_t)MG_TILE;
+    const uint32_t o1 = (n - o0) < (uint32_t)MG_TILE ? n : o0 + (uint32_t)MG_TILE;
+    const PairGeom g = pair_of(o0, n, run);
+    const uint32_t a0 = part[i];
+    const uint32_t a1 = (o1 - g.pb == g.la + g.lb) ? g.la : part[i + 1];
+    const uint32_t b0 = (o0 - g.pb) - a0, b1 = (o1 - g.pb) - a1;
+    merge_tile<BLOCK, KPT>(src + g.pb, a0, a1, src + g.pb + g.la, b0, b1, dst + o0, flip, sm);
+}
+
+// two separate arrays, diagonal range [d0, d1): part has ntiles+1 entries
+__global__ __launch_bounds__(256) void k_merge_part_ab(const uint32_t *__restrict__ A, uint32_t la,
+                                                       const uint32_t *__restrict__ B, uint32_t lb, uint32_t d0,
+                                                       uint32_t d1, uint32_t flip, uint32_t *__restrict__ part,
+                                                       uint32_t ntiles) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i > ntiles) return;
+    uint32_t o = d0 + i * (uint32_t)MG_TILE;
+    if (o > d1 || i == ntiles) o = d1;
+    part[i] = corank(A, la, B, lb, o, flip);
+}
+
+template <int BLOCK, int KPT>
+__global__ __launch_bounds__(BLOCK) void k_merge_ab(const uint32_t *__restrict__ A, const uint32_t *__restrict__ B,
+                                                    uint32_t *__restrict__ out, uint32_t d0, uint32_t d1,
+                                                    uint32_t flip, const uint32_t *__restrict__ part) {
+    __shared__ MgSmem sm;
+    const uint32_t i = blockIdx.x;
+    const uint32_t o0 = d0 + i * (uint32_t)MG_TILE;
+    const uint32_t o1 = (d1 - o0) < (uint32_t)MG_TILE ? d1 : o0 + (uint32_t)MG_TILE;
+    const uint32_t a0 = part[i], a1 = part[i + 1];
+    merge_tile<BLOCK, KPT>(A, a0, a1, B, o0 - a0, o1 - a1, out + (o0 - d0), flip, sm);
+}
+
+// ---------------------------------------------------------------------------------
+// verification helper
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_count_descents(const uint32_t *__restrict__ keys, size_t n, uint32_t flip,
+                                                        uint32_t *__restrict__ count) {
+    __shared__ uint32_t ws[4];
+    uint32_t c = 0;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride)
+        c += ((keys[i] ^ flip) > (keys[i + 1] ^ flip)) ? 1u : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    if ((threadIdx.x & 63u) == 0) ws[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t s = ws[0] + ws[1] + ws[2] + ws[3];
+        if (s) atomicAdd(count, s);
+    }
+}
+
+// =================================================================================
+// host launchers
+// =================================================================================
+static inline unsigned blocks_for(size_t work, unsigned per, unsigned cap) {
+    size_t b = (work + per - 1) / per;
+    if (b < 1) b = 1;
+    if (b > cap) b = cap;
+    return (unsigned)b;
+}
+
+hipError_t launch_fill(uint32_t *out, size_t n, uint64_t seed, int dist, uint64_t param, uint64_t first,
+                       hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_fill<<<blocks_for(n, 256 * 8, 8192), 256, 0, s>>>(out, n, seed, dist, param, first);
+    return hipGetLastError();
+}
+
+hipError_t launch_histogram(const uint32_t *keys, size_t n, uint32_t flip, int bits, uint32_t *hist,
+                            hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = blocks_for(n, 16384, 256);
+    if (bits == 8) k_histogram<8><<<g, HIST_BLOCK, 0, s>>>(keys, n, flip, hist);
+    else if (bits == 1) k_histogram<1><<<g, HIST_BLOCK, 0, s>>>(keys, n, flip, hist);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_plan(const uint32_t *hist, size_t n, int bits, int in_is_out, Plan *plan, hipStream_t s) {
+    k_plan<<<1, 256, 0, s>>>(hist, (uint32_t)n, bits, in_is_out, plan);
+    return hipGetLastError();
+}
+
+hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t n, uint32_t flip,
+                           const uint32_t *hist, uint32_t *lookback, uint32_t *counter, uint32_t *err,
+                           hipStream_t s) {
+    const unsigned g = (unsigned)((n + OS_TILE - 1) / OS_TILE);
+    if (bits == 8)
+        k_onesweep<8, OS_BLOCK, OS_KPT><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback,
+                                                               counter, err);
+    else if (bits == 1)
+        k_onesweep<1, OS_BLOCK, OS_KPT><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback,
+                                                               counter, err);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) {
+    k_final_copy<<<blocks_for(n, 256 * 16, 4096), 256, 0, s>>>(b, plan, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)((n + TS_TILE - 1) / TS_TILE);
+    k_tile_sort<TS_BLOCK, TS_KPT><<<g, TS_BLOCK, 0, s>>>(in, out, (uint32_t)n, flip);
+    return hipGetLastError();
+}
+
+hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)((n + 255) / 256);
+    k_wave_split<<<g, 256, 0, s>>>(keys, (uint32_t)n, flip);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t run, uint32_t flip,
+                             uint32_t *part, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t ntiles = (uint32_t)((n + MG_TILE - 1) / MG_TILE);
+    k_merge_part_pass<<<(ntiles + 255) / 256, 256, 0, s>>>(in, (uint32_t)n, (uint32_t)run, flip, part, ntiles);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_merge_pass<MG_BLOCK, MG_KPT><<<ntiles, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size_t lb, uint32_t *out, size_t d0,
+                           size_t d1, uint32_t flip, uint32_t *part, hipStream_t s) {
+    if (d1 <= d0) return hipSuccess;
+    const uint32_t ntiles = (uint32_t)((d1 - d0 + MG_TILE - 1) / MG_TILE);
+    k_merge_part_ab<<<(ntiles + 1 + 255) / 256, 256, 0, s>>>(a, (uint32_t)la, b, (uint32_t)lb, (uint32_t)d0,
+                                                              (uint32_t)d1, flip, part, ntiles);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_merge_ab<MG_BLOCK, MG_KPT><<<ntiles, MG_BLOCK, 0, s>>>(a, b, out, (uint32_t)d0, (uint32_t)d1, flip, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_count_descents(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *count, hipStream_t s) {
+    if (n < 2) return hipSuccess;
+    k_count_descents<<<blocks_for(n, 256 * 16, 4096), 256, 0, s>>>(keys, n, flip, count);
+    return hipGetLastError();
+}
+
+}  // namespace labsort

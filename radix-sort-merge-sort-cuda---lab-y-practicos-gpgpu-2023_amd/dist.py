@@ -1,0 +1,168 @@
+"""Multi-GPU merge sort: one process per GPU, pairwise merge-split over RCCL/xGMI.
+
+The reference runs on one GPU only (run.sh:11); the north_star partitions n over
+the GPUs of one node for the merge-sort path: every rank sorts its shard locally,
+then a bitonic network of pairwise *merge-split* steps (Baudet & Stevenson's
+block form of Batcher's network: compare-exchange replaced by "merge my block
+with my partner's, keep the lower or the upper half") leaves rank r holding
+global ranks [r*m, (r+1)*m) of the sorted array.  The merge-split step is the
+reference's merge (lab.cu:144-182, A before B on ties) restricted to one half of
+the output diagonal (`labsort_merge` with [0,m) or [m,2m)).
+
+Each step exchanges shards with ONE partner over torch.distributed point-to-point
+send/recv (backend "nccl" = RCCL on ROCm, one xGMI link per pair); log2(p)*(log2(p)+1)/2
+steps for p ranks.  `partial=True` moves only the keys that cross: both sides
+first swap a strided sample of their shards, bracket the split point, swap the
+bracketing window, agree on the exact split k, then send k keys each way.
+
+Local operations are pluggable (`Ops`): the product uses liblabsort.so on the
+rank's GPU (`HipOps`); the CPU tests inject an oracle-backed implementation so the
+exchange schedule is exercised with the gloo backend on machines without GPUs.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.distributed as dist
+
+
+class Ops:
+    """Local operations the exchange schedule needs (all keys int32-viewed uint32/int32)."""
+
+    def local_sort(self, t: torch.Tensor) -> torch.Tensor:  # returns sorted copy (or in place)
+        raise NotImplementedError
+
+    def merge(self, a: torch.Tensor, b: torch.Tensor, d0: int, d1: int) -> torch.Tensor:
+        """elements d0..d1-1 of merge(a, b), a before b on ties"""
+        raise NotImplementedError
+
+    def key_le(self, x: int, y: int) -> bool:
+        raise NotImplementedError
+
+
+class HipOps(Ops):
+    """liblabsort.so on the current GPU."""
+
+    def __init__(self, ls, key: str = "u32", local_algo: str = "radix", stream=None):
+        self.ls, self.key, self.algo, self.stream = ls, key, local_algo, stream
+        self._ws = None
+        self._part = None
+
+    def _workspace(self, n):
+        need = max(self.ls.workspace_bytes(n, self.algo), 256)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device="cuda")
+        return self._ws
+
+    def local_sort(self, t):
+        ws = self._workspace(t.numel())
+        self.ls.sort_device(t, t, t.numel(), key=self.key, algo=self.algo, workspace=ws, stream=self.stream)
+        return t
+
+    def merge(self, a, b, d0, d1):
+        out = torch.empty(max(d1 - d0, 1), dtype=torch.int32, device=a.device if a.numel() else b.device)
+        parts = self.ls.merge_parts(d1 - d0)
+        if self._part is None or self._part.numel() < parts:
+            self._part = torch.empty(parts, dtype=torch.int32, device=out.device)
+        self.ls.merge(a, a.numel(), b, b.numel(), out, d0, d1, self._part, key=self.key, stream=self.stream)
+        return out[: d1 - d0]
+
+    def key_le(self, x, y):
+        f = 0x80000000 if self.key == "i32" else 0
+        return ((x & 0xFFFFFFFF) ^ f) <= ((y & 0xFFFFFFFF) ^ f)
+
+
+def _exchange(send: torch.Tensor, recv: torch.Tensor, partner: int, group=None) -> None:
+    ops = [dist.P2POp(dist.isend, send, partner, group=group), dist.P2POp(dist.irecv, recv, partner, group=group)]
+    for r in dist.batch_isend_irecv(ops):
+        r.wait()
+
+
+def schedule(world: int):
+    """(stage, step) pairs of the bitonic network over `world` ranks (power of two)."""
+    stages = int(math.log2(world))
+    return [(s, t) for s in range(stages) for t in range(s, -1, -1)]
+
+
+def partner_and_side(rank: int, stage: int, step: int):
+    partner = rank ^ (1 << step)
+    ascending = ((rank >> (stage + 1)) & 1) == 0
+    keep_low = (rank < partner) == ascending
+    return partner, keep_low
+
+
+def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, stride: int, group=None) -> int:
+    """Number k of keys that cross: the low side gives its top k, the high side its
+    bottom k.  With L = low side's block and H = high side's block (both sorted, m
+    keys), k = #H among the m smallest of L u H (L first on ties) = m - corank_L(m).
+    Found with two small exchanges: a strided sample, then the bracketing window."""
+    m = mine.numel()
+    # predicate P(i) = L[i] <= H[m-1-i] is true then false; corank = first false i.
+    # low side samples L[j*stride]; high side samples H[m-1-j*stride].
+    idx = torch.arange(0, m, stride, device=mine.device)
+    if keep_low:
+        samp = mine[idx]
+    else:
+        samp = mine[(m - 1) - idx]
+    other = torch.empty_like(samp)
+    _exchange(samp.contiguous(), other, partner, group)
+    Ls, Hs = (samp, other) if keep_low else (other, samp)
+    Lh, Hh = Ls.cpu().tolist(), Hs.cpu().tolist()
+    # first sample j with P(j*stride) false
+    j = 0
+    while j < len(Lh) and ops.key_le(Lh[j], Hh[j]):
+        j += 1
+    lo = 0 if j == 0 else (j - 1) * stride + 1  # P(lo-1) true (or lo = 0)
+    hi = m if j == len(Lh) else j * stride      # P(hi) false (or hi = m)
+    # window: L[lo:hi] and H[m-1-(hi-1) : m-1-lo+1] = H[m-hi : m-lo]
+    if hi > lo:
+        if keep_low:
+            win = mine[lo:hi].contiguous()
+        else:
+            win = mine[m - hi:m - lo].contiguous()
+        owin = torch.empty_like(win)
+        _exchange(win, owin, partner, group)
+        Lw, Hw = (win, owin) if keep_low else (owin, win)
+        Lw, Hw = Lw.cpu().tolist(), Hw.cpu().tolist()
+        # P(i) = L[i] <= H[m-1-i], i in [lo, hi): L[i] = Lw[i-lo], H[m-1-i] = Hw[(m-1-i)-(m-hi)] = Hw[hi-1-i]
+        c = lo
+        while c < hi and ops.key_le(Lw[c - lo], Hw[hi - 1 - c]):
+            c += 1
+    else:
+        c = lo
+    return m - c
+
+
+def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, stride: int = 4096,
+              timings: dict | None = None) -> torch.Tensor:
+    """Sort the global array whose rank-r shard is `local` (equal shard sizes).
+    Returns this rank's shard of the sorted array (global ranks r*m .. r*m+m-1)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if world & (world - 1):
+        raise ValueError("dist_sort: world size must be a power of two")
+    a = ops.local_sort(local)
+    m = a.numel()
+    for stage, step in schedule(world):
+        partner, keep_low = partner_and_side(rank, stage, step)
+        if not partial:
+            b = torch.empty_like(a)
+            _exchange(a.contiguous(), b, partner, group)
+            lo_blk, hi_blk = (a, b) if rank < partner else (b, a)  # same merge order on both sides
+            a = ops.merge(lo_blk, hi_blk, 0, m) if keep_low else ops.merge(lo_blk, hi_blk, m, 2 * m)
+            continue
+        k = _split_count(ops, a, partner, keep_low, stride, group)
+        if k == 0:
+            continue
+        if keep_low:
+            give = a[m - k:].contiguous()   # my top k go up
+        else:
+            give = a[:k].contiguous()       # my bottom k go down
+        got = torch.empty_like(give)
+        _exchange(give, got, partner, group)
+        if keep_low:
+            a = ops.merge(a[:m - k], got, 0, m)   # keep my bottom m-k + partner's bottom k
+        else:
+            a = ops.merge(got, a[k:], 0, m)       # partner's top k + my top m-k
+    return a

@@ -1,0 +1,239 @@
+"""GPU parity tests: every path through liblabsort.so's C-ABI against the oracle
+(std::sort, the spec of order_array: letra.pdf p.3) on the same
+seeded inputs.  Bit-exact equality is the bar (integer work)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+SEED = 0x5EED0000
+
+
+def to_dev(torch, a):
+    a = np.ascontiguousarray(a)
+    return torch.from_numpy(a.view(np.int32).copy()).cuda()
+
+
+def from_dev(t, dtype=np.uint32):
+    return t.cpu().numpy().view(dtype)
+
+
+def ref_sort(oracle, a, key):
+    return oracle.sort_i32(a.view(np.int32)).view(np.uint32) if key == "i32" else oracle.sort_u32(a)
+
+
+# ---- generator ------------------------------------------------------------------------
+@pytest.mark.parametrize("dist", ["u32", "u31", "mod100", "mod1000", "sorted", "reversed", "const", "lowbits"])
+def test_fill_matches_oracle_generator(ls, oracle, torch_gpu, dist):
+    torch = torch_gpu
+    n, first = 100_003, 12_345
+    param = 77 if dist in ("const",) else (13 if dist == "lowbits" else 0)
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, SEED + 1, dist, param=param, first=first)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(from_dev(t), oracle.gen(n, SEED + 1, dist, param=param, first=first))
+
+
+# ---- radix_sort_kernel's job: 64-key tiles by bit splits ---------------------------------
+@pytest.mark.parametrize("key", ["u32", "i32"])
+@pytest.mark.parametrize("dist", ["u32", "mod100", "sorted", "reversed"])
+def test_wave_tile_sort(ls, oracle, torch_gpu, key, dist):
+    torch = torch_gpu
+    n = (1 << 16) + 37
+    a = oracle.gen(n, SEED + 2, dist)
+    t = to_dev(torch, a)
+    ls.wave_tile_sort(t, n, key=key)
+    torch.cuda.synchronize()
+    got = from_dev(t)
+    for s in range(0, n, 64):
+        np.testing.assert_array_equal(got[s:s + 64], ref_sort(oracle, a[s:s + 64].copy(), key))
+
+
+# ---- LDS tile sort (stage 1+2 counterpart) ---------------------------------------------
+@pytest.mark.parametrize("key", ["u32", "i32"])
+@pytest.mark.parametrize("dist", ["u32", "mod100", "const", "lowbits"])
+def test_tile_sort(ls, oracle, torch_gpu, key, dist):
+    torch = torch_gpu
+    T = ls.tile_keys()
+    n = 5 * T + 1234
+    a = oracle.gen(n, SEED + 3, dist, param=9)
+    t = to_dev(torch, a)
+    o = torch.empty_like(t)
+    ls.tile_sort(t, o, n, key=key)
+    torch.cuda.synchronize()
+    got = from_dev(o)
+    for s in range(0, n, T):
+        np.testing.assert_array_equal(got[s:s + T], ref_sort(oracle, a[s:s + T].copy(), key))
+
+
+# ---- digit histogram ----------------------------------------------------------------------
+@pytest.mark.parametrize("bits", [8, 1])
+@pytest.mark.parametrize("key", ["u32", "i32"])
+def test_histogram(ls, oracle, torch_gpu, bits, key):
+    torch = torch_gpu
+    n = 1_000_003
+    a = oracle.gen(n, SEED + 4, "u32")
+    t = to_dev(torch, a)
+    R, P = 1 << bits, (32 + bits - 1) // bits
+    h = torch.zeros(P * R, dtype=torch.int32, device="cuda")
+    ls.histogram(t, n, h, bits=bits, key=key)
+    torch.cuda.synchronize()
+    got = from_dev(h).reshape(P, R)
+    x = a ^ np.uint32(0x80000000) if key == "i32" else a
+    for p in range(P):
+        d = (x >> np.uint32(p * bits)) & np.uint32(R - 1)
+        np.testing.assert_array_equal(got[p], np.bincount(d, minlength=R).astype(np.uint32))
+
+
+# ---- whole sorts ----------------------------------------------------------------------------
+SIZES = [1, 2, 63, 64, 65, 1000, 8191, 8192, 8193, 65536, 100_000, (1 << 20) + 12345]
+DISTS = ["u32", "u31", "mod100", "mod1000", "sorted", "reversed", "const", "lowbits"]
+
+
+@pytest.mark.parametrize("algo", ["radix", "merge"])
+@pytest.mark.parametrize("key", ["u32", "i32"])
+@pytest.mark.parametrize("n", SIZES)
+def test_sort_device_uniform(ls, oracle, torch_gpu, algo, key, n):
+    torch = torch_gpu
+    a = oracle.gen(n, SEED + 5 + n, "u32")
+    t = to_dev(torch, a)
+    o = torch.empty_like(t)
+    ls.sort_device(t, o, n, key=key, algo=algo)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key))
+    np.testing.assert_array_equal(from_dev(t), a)  # input untouched
+
+
+@pytest.mark.parametrize("algo", ["radix", "merge"])
+@pytest.mark.parametrize("dist", DISTS)
+@pytest.mark.parametrize("inplace", [False, True])
+def test_sort_device_distributions(ls, oracle, torch_gpu, algo, dist, inplace):
+    torch = torch_gpu
+    n = 300_007
+    a = oracle.gen(n, SEED + 6, dist, param=(0xABCDEF if dist == "const" else 11))
+    for key in ("u32", "i32"):
+        t = to_dev(torch, a)
+        o = t if inplace else torch.empty_like(t)
+        ls.sort_device(t, o, n, key=key, algo=algo)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key), err_msg=f"{key}")
+
+
+@pytest.mark.parametrize("n", [1000, 8193, 70_000])
+@pytest.mark.parametrize("key", ["u32", "i32"])
+def test_sort_device_radix1(ls, oracle, torch_gpu, n, key):
+    """letra.pdf's literal form: 32 one-bit split passes."""
+    torch = torch_gpu
+    a = oracle.gen(n, SEED + 7, "u32")
+    t = to_dev(torch, a)
+    o = torch.empty_like(t)
+    ls.sort_device(t, o, n, key=key, algo="radix1")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key))
+
+
+def test_sort_device_offsets_unaligned(ls, oracle, torch_gpu):
+    """Sub-tensor views (pointer not 16-B aligned) go through the scalar paths."""
+    torch = torch_gpu
+    n = 200_001
+    a = oracle.gen(n + 3, SEED + 8, "u32")
+    t = to_dev(torch, a)
+    o = torch.zeros_like(t)
+    for algo in ("radix", "merge"):
+        ls.sort_device(t[1:1 + n], o[3:3 + n - 2], n - 2, algo=algo)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(from_dev(o)[3:3 + n - 2], oracle.sort_u32(a[1:n - 1]))
+
+
+# ---- merge building blocks ------------------------------------------------------------------
+def test_merge_pass(ls, oracle, torch_gpu):
+    torch = torch_gpu
+    run = 8192
+    n = 5 * run + 777
+    a = oracle.gen(n, SEED + 9, "mod1000")
+    runs = np.concatenate([oracle.sort_u32(a[s:s + run]) for s in range(0, n, run)])
+    t = to_dev(torch, runs)
+    o = torch.empty_like(t)
+    part = torch.empty(ls.merge_parts(n), dtype=torch.int32, device="cuda")
+    ls.merge_pass(t, o, n, run, part)
+    torch.cuda.synchronize()
+    got = from_dev(o)
+    for s in range(0, n, 2 * run):
+        np.testing.assert_array_equal(got[s:s + 2 * run], oracle.sort_u32(a[s:s + 2 * run]))
+
+
+@pytest.mark.parametrize("la,lb", [(0, 5000), (5000, 0), (1, 1), (70_000, 30_001), (4096, 4096)])
+def test_merge_diagonal_ranges(ls, oracle, torch_gpu, la, lb):
+    """merge-split step of the multi-GPU exchange: a diagonal range of merge(A,B)."""
+    torch = torch_gpu
+    A = oracle.sort_u32(oracle.gen(la, SEED + 10, "mod1000"))
+    B = oracle.sort_u32(oracle.gen(lb, SEED + 11, "mod1000"))
+    tA = to_dev(torch, A) if la else torch.empty(1, dtype=torch.int32, device="cuda")
+    tB = to_dev(torch, B) if lb else torch.empty(1, dtype=torch.int32, device="cuda")
+    tot = la + lb
+    for d0, d1 in [(0, tot), (0, tot // 2), (tot // 2, tot), (tot // 3, tot // 3 + 5000)]:
+        d1 = min(d1, tot)
+        if d1 <= d0:
+            continue
+        out = torch.empty(d1 - d0, dtype=torch.int32, device="cuda")
+        part = torch.empty(ls.merge_parts(d1 - d0), dtype=torch.int32, device="cuda")
+        ls.merge(tA, la, tB, lb, out, d0, d1, part)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(from_dev(out), oracle.merge_split(A, B, d0, d1))
+
+
+# ---- host-pointer drop-ins (lab.h) ------------------------------------------------------------
+@pytest.mark.parametrize("n", [256, 1024, 65536, 1 << 17, 1 << 20])
+def test_order_array_matches_std_sort(ls, oracle, torch_gpu, n):
+    a = oracle.gen(n, SEED + 12, "mod100").astype(np.int32)  # main.cpp:10 data shape
+    b = a.copy()
+    ls.order_array(b)
+    np.testing.assert_array_equal(b, np.sort(a))
+
+
+def test_order_array_negative_keys(ls, oracle, torch_gpu):
+    """Outside the reference's domain (F6: it hangs); we sort signed order."""
+    a = oracle.gen(100_000, SEED + 13, "u32").view(np.int32).copy()
+    b = a.copy()
+    ls.order_array(b)
+    np.testing.assert_array_equal(b, np.sort(a))
+
+
+def test_order_with_trust(ls, oracle):
+    a = oracle.gen(65536, SEED + 14, "mod1000").astype(np.int32)
+    b = a.copy()
+    ls.order_with_trust(b)
+    np.testing.assert_array_equal(b, np.sort(a))
+
+
+@pytest.mark.parametrize("algo", ["radix", "merge", "radix1"])
+def test_sort_host_algorithms(ls, oracle, torch_gpu, algo):
+    a = oracle.gen(123_457, SEED + 15, "u32")
+    b = a.copy()
+    ls.sort_host(b, algo=algo)
+    np.testing.assert_array_equal(b, oracle.sort_u32(a))
+
+
+def test_count_descents(ls, oracle, torch_gpu):
+    torch = torch_gpu
+    a = np.arange(10_000, dtype=np.uint32)
+    a[[10, 500, 9000]] = 0
+    t = to_dev(torch, a)
+    c = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ls.count_descents(t, a.size, c)
+    torch.cuda.synchronize()
+    assert int(c.item()) == 3
+
+
+def test_timing_hooks(ls, oracle, torch_gpu):
+    torch = torch_gpu
+    n = 1 << 20
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, SEED, "u32")
+    o = torch.empty_like(t)
+    ls.timing_enable(True)
+    ls.sort_device(t, o, n, algo="radix")
+    torch.cuda.synchronize()
+    ms, cnt = ls.timing_read("onesweep")
+    ls.timing_enable(False)
+    assert cnt == 4 and ms > 0
