@@ -1,0 +1,258 @@
+"""bench.py -- BASELINE.json's headline metric: Mkeys/s sorting uint32 keys.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--algo radix|merge] [--log2n 28]
+
+N = 1: one "step" is one device-resident sort of n = 2^28 uniform uint32 keys
+(BASELINE config 3: radix, 1 MI355X) through liblabsort's C-ABI
+(`labsort_sort_device`, the stages of order_array between its H2D and D2H
+copies, lab.cu:321-397).  Keys are generated on the device (counter-based
+generator, seed 0x5EED0003) and stay resident in HBM; the sort is out of place
+so every step sorts the same input.
+
+N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): the
+merge-sort path of the north_star.  Each rank holds a fixed 2^log2n-key shard
+(weak scaling), sorts it locally with the radix kernels, then the pairwise
+merge-split network exchanges keys over RCCL send/recv (dist.py).  value = all
+ranks' keys / max-over-ranks time.
+
+After the timed region the output is verified with size-independent properties
+(no descents, same sum / sum of squares / digit histograms as the input);
+a failed check aborts the bench.  The printed JSON line carries:
+  roofline     the dominant kernel (radix: the onesweep scatter pass) -- achieved
+               = algorithmic bytes per launch (8 B/key: read + write each key once)
+               / average launch duration from HIP events recorded on the sort's
+               stream during the timed region; traffic = HBM bytes per launch from
+               the committed rocprofv3 PMC pass (profiles/), or null.
+  cpu_baseline std::sort (the oracle: oracle/cpu_sort.cpp) on one host core over a
+               bounded sample of the same workload (rank 0, N = 1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import importlib
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG_NAME = "radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SEED = 0x5EED0000
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--algo", default="radix", choices=["radix", "merge", "radix1"])
+    ap.add_argument("--log2n", type=int, default=28, help="keys per GPU = 2^log2n")
+    ap.add_argument("--dist", default="u32")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    return ap.parse_args()
+
+
+def pmc_traffic(kernel_class: str, n: int):
+    """HBM bytes per launch of the dominant kernel from the newest committed PMC
+    summary (profiles/*_pmc.json, written by profiles/pmc_summary.py from separate
+    rocprofv3 --pmc passes, FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM).
+    Only used when the summary was taken on the same n."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        k = d.get("kernels", {}).get(kernel_class)
+        if k and int(d.get("n", -1)) == n and k.get("hbm_bytes_per_launch"):
+            return float(k["hbm_bytes_per_launch"]), os.path.relpath(f, REPO)
+    return None, None
+
+
+def verify(torch, ls, src, out, n, key):
+    """Size-independent checks: out is sorted and a permutation of src (multiset
+    fingerprints: sum, sum of squares mod 2^64, 8-bit digit histograms)."""
+    cnt = torch.zeros(1, dtype=torch.int32, device=out.device)
+    ls.count_descents(out, n, cnt, key=key)
+    hs = torch.zeros(4 * 256, dtype=torch.int32, device=out.device)
+    ho = torch.zeros(4 * 256, dtype=torch.int32, device=out.device)
+    ls.histogram(src, n, hs, bits=8, key=key)
+    ls.histogram(out, n, ho, bits=8, key=key)
+
+    def fp(t):
+        v = t.to(torch.int64) & 0xFFFFFFFF
+        s1 = int(v.sum().item())
+        s2 = int((v * v).sum().item())  # wraps mod 2^64: a fingerprint, not a value
+        return s1, s2
+
+    ok = int(cnt.item()) == 0 and torch.equal(hs, ho) and fp(src) == fp(out)
+    return ok, int(cnt.item())
+
+
+def cpu_baseline(budget_s: float):
+    """std::sort (oracle/cpu_sort.cpp) on 1 core over samples of the same workload:
+    uniform uint32 keys from the same generator, 2^24 keys per sort, repeated until
+    the budget is spent.  Reported as Mkeys/s."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O  # test infrastructure: the CPU baseline leg only
+
+    ns = 1 << 24
+    keys = O.gen(ns, SEED + 3, "u32")
+    t = 0.0
+    reps = 0
+    while t < budget_s and reps < 64:
+        t += O.time_sort_u32(keys, threads=1, reps=1)
+        reps += 1
+    return {"value": round(ns * reps / t / 1e6, 2), "unit": "Mkeys/s", "cores": 1, "kind": "port",
+            "sample": f"std::sort of {reps} x 2^24 uniform uint32 keys (same generator, seed 0x5EED0003), "
+                      f"{t:.1f} s on one host core"}
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if args.gpus > 1 and world == 1:
+            sys.exit("bench.py: --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if REPO not in sys.path:
+        sys.path.insert(0, REPO)
+    ls = importlib.import_module(PKG_NAME)
+
+    n = 1 << args.log2n
+    key = "u32"
+    stream = torch.cuda.Stream(device=dev)
+    ws = None
+
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        dmod = importlib.import_module(PKG_NAME + ".dist")
+        ops = dmod.HipOps(ls, key=key, local_algo="radix", stream=stream)
+        src = torch.empty(n, dtype=torch.int32, device=dev)
+        with torch.cuda.stream(stream):
+            ls.fill(src, n, SEED + 5, args.dist, first=rank * n, stream=stream)
+
+        def step():
+            with torch.cuda.stream(stream):
+                return dmod.dist_sort(src, ops, copy_input=True)
+
+        def barrier():
+            dist.barrier()
+    else:
+        src = torch.empty(n, dtype=torch.int32, device=dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        ws = torch.empty(max(ls.workspace_bytes(n, args.algo), 256), dtype=torch.uint8, device=dev)
+        ls.fill(src, n, SEED + 3, args.dist, stream=stream)
+
+        def step():
+            ls.sort_device(src, out, n, key=key, algo=args.algo, workspace=ws, stream=stream)
+            return out
+
+        def barrier():
+            pass
+
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+
+    dom = "onesweep" if args.algo in ("radix", "radix1") else "merge"
+    ls.timing_enable(True)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    k_ms, k_cnt = ls.timing_read(dom)
+    ls.timing_enable(False)
+    elapsed = t1 - t0
+
+    if world > 1:
+        import torch.distributed as dist
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        # global check: every shard sorted, boundaries ordered, multiset preserved
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        ls.count_descents(res, n, cnt, key=key)
+        edges = torch.stack([res[0], res[-1]]).to(torch.int64) & 0xFFFFFFFF
+        allg = [torch.empty_like(edges) for _ in range(world)]
+        dist.all_gather(allg, edges)
+        h_in = torch.zeros(1024, dtype=torch.int32, device=dev)
+        h_out = torch.zeros(1024, dtype=torch.int32, device=dev)
+        ls.histogram(src, n, h_in, key=key)
+        ls.histogram(res, n, h_out, key=key)
+        s_in = (src.to(torch.int64) & 0xFFFFFFFF).sum()
+        s_out = (res.to(torch.int64) & 0xFFFFFFFF).sum()
+        red = torch.stack([s_in, s_out])
+        dist.all_reduce(h_in)
+        dist.all_reduce(h_out)
+        dist.all_reduce(red)
+        ok = int(cnt.item()) == 0 and torch.equal(h_in, h_out) and int(red[0]) == int(red[1])
+        ok = ok and all(int(allg[i][1]) <= int(allg[i + 1][0]) for i in range(world - 1))
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+        ok = bool(okt.item())
+    else:
+        ok, desc = verify(torch, ls, src, res, n, key)
+    if not ok:
+        print(f"bench.py: rank {rank}: OUTPUT CHECK FAILED (sort result is not a sorted permutation)",
+              file=sys.stderr)
+        sys.exit(3)
+
+    total_keys = n * world * args.steps
+    value = total_keys / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    if rank == 0:
+        avg_ms = k_ms / k_cnt if k_cnt else None
+        per_launch_bytes = 8.0 * n if dom == "onesweep" else 8.0 * n
+        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms else None
+        traffic, tsrc = pmc_traffic(dom, n)
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                    "traffic": traffic, "kernel": f"k_{dom}", "launches": k_cnt,
+                    "avg_launch_ms": round(avg_ms, 5) if avg_ms else None,
+                    "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_seconds)
+        wl = {"radix": "LSD radix sort (8-bit digits, onesweep)", "merge": "LDS tile sort + merge-path passes",
+              "radix1": "LSD radix with 1-bit split passes (letra.pdf)"}[args.algo]
+        if world > 1:
+            workload = (f"merge sort across {world} GPUs: local radix sort of 2^{args.log2n} uint32 keys per GPU "
+                        f"+ pairwise merge-split over RCCL (BASELINE config 5 shape, weak scaling)")
+        else:
+            workload = f"{wl}, n=2^{args.log2n} uint32 {args.dist}, device-resident (BASELINE config 3)"
+        line = {
+            "metric": "Mkeys/s sorting uint32, n=2^28, 1 GPU (+ merge-sort at 2/4/8)",
+            "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+            "data": "synthetic (counter-based splitmix64 generator on device)",
+            "config": {"workload": workload, "n_per_gpu": n, "algo": args.algo if world == 1 else "merge",
+                       "key": key, "dist": args.dist,
+                       "parallelism": "single GPU" if world == 1 else f"{world} ranks, RCCL pairwise merge-split"},
+            "verified": "sorted permutation (descents, digit histograms, sums)",
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -30,7 +30,8 @@ import torch.distributed as dist
 class Ops:
     """Local operations the exchange schedule needs (all keys int32-viewed uint32/int32)."""
 
-    def local_sort(self, t: torch.Tensor) -> torch.Tensor:  # returns sorted copy (or in place)
+    def local_sort(self, t: torch.Tensor, out_of_place: bool = False) -> torch.Tensor:
+        """Sorted keys of t: in place, or into a new tensor when out_of_place."""
         raise NotImplementedError
 
     def merge(self, a: torch.Tensor, b: torch.Tensor, d0: int, d1: int) -> torch.Tensor:
@@ -55,10 +56,11 @@ class HipOps(Ops):
             self._ws = torch.empty(need, dtype=torch.uint8, device="cuda")
         return self._ws
 
-    def local_sort(self, t):
+    def local_sort(self, t, out_of_place=False):
         ws = self._workspace(t.numel())
-        self.ls.sort_device(t, t, t.numel(), key=self.key, algo=self.algo, workspace=ws, stream=self.stream)
-        return t
+        out = torch.empty_like(t) if out_of_place else t
+        self.ls.sort_device(t, out, t.numel(), key=self.key, algo=self.algo, workspace=ws, stream=self.stream)
+        return out
 
     def merge(self, a, b, d0, d1):
         out = torch.empty(max(d1 - d0, 1), dtype=torch.int32, device=a.device if a.numel() else b.device)
@@ -135,14 +137,15 @@ def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, str
 
 
 def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, stride: int = 4096,
-              timings: dict | None = None) -> torch.Tensor:
+              copy_input: bool = False) -> torch.Tensor:
     """Sort the global array whose rank-r shard is `local` (equal shard sizes).
-    Returns this rank's shard of the sorted array (global ranks r*m .. r*m+m-1)."""
+    Returns this rank's shard of the sorted array (global ranks r*m .. r*m+m-1).
+    `local` is sorted in place unless copy_input (then it is left untouched)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     if world & (world - 1):
         raise ValueError("dist_sort: world size must be a power of two")
-    a = ops.local_sort(local)
+    a = ops.local_sort(local, out_of_place=copy_input)
     m = a.numel()
     for stage, step in schedule(world):
         partner, keep_low = partner_and_side(rank, stage, step)
