@@ -1,0 +1,125 @@
+"""CPU tests of the drop-in boundary: liblabsort.so loads, exports every symbol
+include/*.h declares (C names unmangled, lab.h's two with the reference's C++
+mangling), the host-side argument checks and sizing functions behave, and the
+reference's own main.cpp / performanceTest.cpp were compiled unchanged against
+include/lab.h and link liblabsort.so.  No kernel is launched."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd")
+LIB = os.path.join(PKG, "liblabsort.so")
+
+
+def exported():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], check=True, capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if line.strip()}
+
+
+def header_functions(path):
+    txt = open(path).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    txt = re.sub(r"//[^\n]*", "", txt)
+    return re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b([A-Za-z_]\w*)\s*\([^;{]*\)\s*;", txt, flags=re.M)
+
+
+def test_library_built():
+    assert os.path.exists(LIB), "liblabsort.so missing: run __graft_entry__.build()"
+
+
+def test_labsort_h_symbols_exported():
+    names = header_functions(os.path.join(REPO, "include", "labsort.h"))
+    assert "labsort_sort_device" in names and "sort" in names and len(names) >= 20
+    missing = [n for n in names if n not in exported()]
+    assert not missing, missing
+
+
+def test_lab_h_cxx_symbols_exported():
+    names = header_functions(os.path.join(REPO, "include", "lab.h"))
+    assert set(names) == {"order_array", "order_with_trust"}
+    ex = exported()
+    # same mangled names as the reference's build of lab.h:9-10
+    assert "_Z11order_arrayPii" in ex and "_Z16order_with_trustPii" in ex
+
+
+def test_utils_h_symbol_exported():
+    assert "labsort_hip_error_string" in exported()
+
+
+def test_python_symbol_list_matches_header(ls):
+    names = set(header_functions(os.path.join(REPO, "include", "labsort.h")))
+    assert names == set(ls.C_SYMBOLS)
+
+
+def test_no_oracle_in_product():
+    """The product never links, loads or imports anything under oracle/."""
+    out = subprocess.run(["ldd", LIB], capture_output=True, text=True).stdout
+    assert "oracle" not in out
+    assert "liboracle" not in open(LIB, "rb").read().decode("latin1")
+    for root, _, files in os.walk(PKG):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h", ".cpp")):
+                src = open(os.path.join(root, f)).read()
+                assert not re.search(r"^\s*(import|from)\s+oracle", src, flags=re.M), f
+                assert "liboracle" not in src, f
+
+
+# ---- host logic (no device calls) ------------------------------------------------------
+def test_sizes_and_limits(ls):
+    assert ls.tile_keys() == 8192 and ls.merge_tile_keys() == 4096
+    assert ls.max_keys("radix") == (1 << 30) - 1
+    assert ls.max_keys("merge") == 2**31 - 1
+    assert ls.merge_parts(0) == 2 and ls.merge_parts(4096) == 3 and ls.merge_parts(4097) == 4
+    for algo in ("radix", "merge", "radix1"):
+        prev = 0
+        for n in (1, 100, 8192, 8193, 1 << 20, 1 << 28):
+            w = ls.workspace_bytes(n, algo)
+            assert w >= prev
+            prev = w
+            if n > 8192:
+                assert w >= 4 * n  # one ping-pong buffer of n keys
+    # radix at 2^28: tmp keys + 4 passes x 32768 tiles x 256 look-back words + hist
+    assert ls.workspace_bytes(1 << 28, "radix") < 4 * (1 << 28) + 4 * 32768 * 256 * 4 + (1 << 20)
+
+
+def test_argument_errors(ls):
+    L = ls.lib
+    ws = ctypes.create_string_buffer(1 << 16)
+    assert L.labsort_sort_device(None, None, 0, 0, 0, None, 0, None) == ls.OK  # n = 0: nothing to do
+    assert L.labsort_sort_device(None, None, 10, 0, 0, ws, 1 << 16, None) == ls.ERR_ARG
+    p = ctypes.addressof(ws)
+    assert L.labsort_sort_device(p, p, 10, 7, 0, p, 1 << 16, None) == ls.ERR_ARG  # bad key type
+    assert L.labsort_sort_device(p, p, 10, 0, 9, p, 1 << 16, None) == ls.ERR_ARG  # bad algo
+    assert L.labsort_sort_device(p, p, 1 << 20, 0, 0, p, 16, None) == ls.ERR_ARG  # workspace too small
+    assert L.labsort_sort_device(p, p, 1 << 30, 0, 0, p, 1 << 16, None) == ls.ERR_ARG  # > radix max
+    assert L.labsort_merge_pass(p, p, 100, 8192, 0, p, None) == ls.ERR_ARG  # in == out
+    assert L.labsort_merge_pass(p, p + 4, 100, 1000, 0, p, None) == ls.ERR_ARG  # run not a power of two
+    assert L.labsort_merge(p, 5, p, 5, p, 3, 2, 0, p, None) == ls.ERR_ARG  # d1 < d0
+    assert L.labsort_merge(p, 5, p, 5, p, 0, 11, 0, p, None) == ls.ERR_ARG  # d1 > la + lb
+    assert L.labsort_histogram(p, 10, 0, 4, p, None) == ls.ERR_ARG  # bits not 8/1
+    assert L.labsort_fill(p, 10, 1, 99, 0, 0, None) == ls.ERR_ARG
+    assert L.labsort_timing_read(99, None, None) == ls.ERR_ARG
+    assert ls.lib.labsort_error_string(ls.ERR_ARG) == b"invalid argument"
+
+
+def test_python_wrapper_raises(ls):
+    with pytest.raises(ls.LabsortError):
+        ls._check(ls.ERR_ARG, "x")
+
+
+# ---- the reference's harness drivers, compiled unchanged ---------------------------------
+@pytest.mark.parametrize("prog", ["sort", "performaceTest"])
+def test_harness_links_liblabsort(prog):
+    exe = os.path.join(REPO, "harness", "bin", prog)
+    if not os.path.exists(exe):
+        pytest.skip("harness binaries not built (reference sources absent)")
+    und = subprocess.run(["nm", "-u", exe], check=True, capture_output=True, text=True).stdout
+    assert "_Z16order_with_trustPii" in und
+    if prog == "sort":
+        assert "_Z11order_arrayPii" in und
+    ldd = subprocess.run(["ldd", exe], capture_output=True, text=True).stdout
+    assert "liblabsort.so" in ldd and "not found" not in ldd.split("liblabsort.so")[1].splitlines()[0]

@@ -1,0 +1,202 @@
+"""CPU tests of the oracle (test infrastructure) against the committed golden
+fixtures and against independent numpy restatements, plus the documented
+behaviour of the lab.cu restatement.  No GPU needed."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def small():
+    with np.load(os.path.join(GOLD, "small.npz")) as z:  # allow_pickle=False (default)
+        return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="module")
+def big():
+    with open(os.path.join(GOLD, "big.json")) as f:
+        return json.load(f)
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def cases(small):
+    return sorted({k.split("_", 1)[1] for k in small if k.startswith("in_")})
+
+
+# ---- generator -------------------------------------------------------------------------
+def test_generator_reproduces_fixture_inputs(oracle, small):
+    for key in cases(small):
+        dist, n = key.rsplit("_", 1)
+        n = int(n)
+        di = ["u32", "u31", "mod100", "mod1000"].index(dist)
+        seed = 0x5EED1000 + 16 * di + n.bit_length()
+        np.testing.assert_array_equal(oracle.gen(n, seed, dist), small[f"in_{key}"], err_msg=key)
+
+
+def test_generator_formula_python(oracle):
+    """splitmix64 restated in Python: key[i] = hi32(mix(seed ^ i*phi))."""
+    M = (1 << 64) - 1
+
+    def mix(z):
+        z = (z + 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    seed, first = 0x1234, 99
+    got = oracle.gen(50, seed, "u32", first=first)
+    exp = [mix(seed ^ (((first + i) * 0x9E3779B97F4A7C15) & M)) >> 32 for i in range(50)]
+    assert got.tolist() == exp
+    exp31 = [mix(seed ^ (((first + i) * 0x9E3779B97F4A7C15) & M)) >> 33 for i in range(50)]
+    assert oracle.gen(50, seed, "u31", first=first).tolist() == exp31
+    assert (oracle.gen(1000, 7, "mod100") < 100).all() and (oracle.gen(1000, 7, "mod1000") < 1000).all()
+    np.testing.assert_array_equal(oracle.gen(10, 7, "reversed"), np.arange(9, -1, -1, dtype=np.uint32))
+    np.testing.assert_array_equal(oracle.gen(10, 7, "sorted", first=5), np.arange(5, 15, dtype=np.uint32))
+    assert (oracle.gen(100, 7, "lowbits", param=5) < 32).all()
+
+
+def test_generator_shard_consistency(oracle):
+    """A rank's shard (first = r*m) is the slice of the global stream."""
+    full = oracle.gen(4000, 0xABC, "u32")
+    np.testing.assert_array_equal(np.concatenate([oracle.gen(1000, 0xABC, "u32", first=r * 1000)
+                                                  for r in range(4)]), full)
+
+
+# ---- std::sort oracle --------------------------------------------------------------------
+def test_sort_oracle_matches_fixtures(oracle, small):
+    for key in cases(small):
+        a = small[f"in_{key}"]
+        np.testing.assert_array_equal(oracle.sort_u32(a), small[f"sorted_{key}"], err_msg=key)
+        np.testing.assert_array_equal(oracle.sort_i32(a.view(np.int32)).view(np.uint32),
+                                      small[f"sorted_i32_{key}"], err_msg=key)
+        # independent check: numpy's sort
+        np.testing.assert_array_equal(np.sort(a), small[f"sorted_{key}"], err_msg=key)
+
+
+def test_sort_oracle_big_sha(oracle, big):
+    """Full-size fixtures: SHA-256 of input and sorted output (2^16, 2^20 here; the
+    2^28 one is checked on the GPU)."""
+    for name, c in big.items():
+        if c["log2n"] > 20:
+            continue
+        a = oracle.gen(1 << c["log2n"], c["seed"], c["dist"])
+        assert sha(a) == c["sha256_input"], name
+        assert sha(oracle.sort_u32(a)) == c["sha256_sorted_u32"], name
+        if "sha256_sorted_i32" in c:
+            assert sha(oracle.sort_i32(a.view(np.int32))) == c["sha256_sorted_i32"], name
+
+
+def test_parallel_sort_matches(oracle):
+    a = oracle.gen(1 << 18, 77, "mod1000")
+    b = a.copy()
+    oracle.lib().oracle_par_sort_u32(b.ctypes.data, b.size, 4)
+    np.testing.assert_array_equal(b, np.sort(a))
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 300), (0, 150), (150, 300), (77, 201)])
+def test_merge_split_oracle(oracle, lo, hi):
+    A = np.sort(oracle.gen(100, 1, "mod100"))
+    B = np.sort(oracle.gen(200, 2, "mod100"))
+    ref = np.concatenate([A, B])[np.argsort(np.concatenate([A, B]), kind="stable")]
+    np.testing.assert_array_equal(oracle.merge_split(A, B, lo, hi), ref[lo:hi])
+
+
+# ---- restatement of lab.cu ---------------------------------------------------------------
+def test_warp_scan_restatement():
+    import oracle as O
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        v = rng.integers(0, 2, 32).astype(np.int32)
+        np.testing.assert_array_equal(O.labcu_warp_scan(v), np.concatenate([[0], np.cumsum(v)[:-1]]))
+
+
+def test_bsearch_restatement():
+    """busquedaPorBiparticion (lab.cu:102-132): lower_bound when previoAIguales,
+    upper_bound otherwise, relative to the start; size <= 0 -> 0."""
+    import oracle as O
+    arr = np.array([1, 3, 3, 3, 7, 9, 9, 12], dtype=np.int32)
+    for x in range(0, 14):
+        for start, size in [(0, 8), (1, 5), (3, 1), (2, 0)]:
+            seg = arr[start:start + size]
+            lo = int(np.searchsorted(seg, x, "left")) if size > 0 else 0
+            hi = int(np.searchsorted(seg, x, "right")) if size > 0 else 0
+            assert O.labcu_bsearch(arr, start, size, x, True) == lo, (x, start, size)
+            assert O.labcu_bsearch(arr, start, size, x, False) == hi, (x, start, size)
+
+
+def test_restatement_fixtures(small):
+    """The lab.cu restatement's recorded outputs: correct (== std::sort) for every
+    n <= 512; where it is wrong at n >= 1024 that is F5 (see test below)."""
+    import oracle as O
+    n_ok = n_bad = 0
+    for key in cases(small):
+        if key.startswith("u32_"):
+            continue
+        a = small[f"in_{key}"]
+        st, out = O.labcu_order_array(a.view(np.int32))
+        assert O.STATUS_NAMES and {v: k for k, v in O.STATUS_NAMES.items()}[st] == int(small[f"ref_status_{key}"][0])
+        np.testing.assert_array_equal(out.view(np.uint32), small[f"ref_out_{key}"], err_msg=key)
+        n = int(key.rsplit("_", 1)[1])
+        correct = st == "ok" and np.array_equal(out.view(np.uint32), small[f"sorted_{key}"])
+        if n <= 512:
+            assert correct, key
+        n_ok += correct
+        n_bad += not correct
+    assert n_ok > 0 and n_bad > 0  # F5 shows up among the fixtures
+
+
+def test_f5_counter_example():
+    """F5 (lab.cu:253-260): the inclusive search end passed as a size mis-ranks a
+    splitter; the one-line exclusive-end fix sorts correctly."""
+    import oracle as O
+    with np.load(os.path.join(GOLD, "f5.npz")) as z:
+        inp, ref_out, fixed, srt = z["inp"], z["ref_out"], z["fixed_out"], z["sorted"]
+    st, out = O.labcu_order_array(inp.view(np.int32))
+    assert st == "ok"
+    np.testing.assert_array_equal(out.view(np.uint32), ref_out)
+    assert not np.array_equal(ref_out, srt)
+    st, out = O.labcu_order_array(inp.view(np.int32), fix_f5=True)
+    np.testing.assert_array_equal(out.view(np.uint32), fixed)
+    np.testing.assert_array_equal(fixed, srt)
+
+
+@pytest.mark.parametrize("log2n", [10, 12, 14])
+@pytest.mark.parametrize("dist", ["u31", "mod100", "mod1000"])
+def test_restatement_fix_f5_always_correct(oracle, log2n, dist):
+    for s in range(3):
+        a = oracle.gen(1 << log2n, 0x5EED6000 + s, dist)
+        st, out = oracle.labcu_order_array(a.view(np.int32), fix_f5=True)
+        assert st == "ok"
+        np.testing.assert_array_equal(out.view(np.uint32), oracle.sort_u32(a))
+
+
+def test_restatement_f4_launch_failure(oracle):
+    """n >= 2^18: separators_kernel needs > 1024 threads (lab.cu:365-375)."""
+    a = oracle.gen(1 << 18, 1, "mod100")
+    st, _ = oracle.labcu_order_array(a.view(np.int32))
+    assert st == "launch_fail"
+
+
+def test_restatement_f6_negative_keys_hang(oracle):
+    """Negative int keys: radix_sort_kernel never sees a sorted warp (lab.cu:56-84)."""
+    a = np.arange(32, dtype=np.int32)[::-1].copy()
+    a[5] = -7
+    st, _ = oracle.labcu_radix_tiles(a)
+    assert st == "hang"
+
+
+def test_restatement_radix_tiles(oracle):
+    """Stage 1 alone sorts each 32-key tile (non-negative keys)."""
+    a = oracle.gen(32 * 50, 3, "u31").view(np.int32)
+    st, out = oracle.labcu_radix_tiles(a)
+    assert st == "ok"
+    for s in range(0, a.size, 32):
+        np.testing.assert_array_equal(out[s:s + 32], np.sort(a[s:s + 32]))
