@@ -154,8 +154,9 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
     HIP_TRY(launch_plan(hist, n, bits, in == out ? 1 : 0, plan, s));
     for (int p = 0; p < L.P; ++p) {
         TimingScope ts(LABSORT_K_ONESWEEP, s);
-        HIP_TRY(launch_onesweep(b, plan, p, bits, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
-                                counters + p, err, s));
+        uint32_t *lb = lookback + (size_t)p * L.ntiles * L.R;
+        if (bits == 8) HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, hist, lb, counters + p, err, s));
+        else HIP_TRY(launch_onesweep(b, plan, p, bits, n, flip, hist, lb, counters + p, err, s));
     }
     HIP_TRY(launch_final_copy(b, plan, n, s));
     return LABSORT_OK;

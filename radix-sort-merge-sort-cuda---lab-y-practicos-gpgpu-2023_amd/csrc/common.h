@@ -15,6 +15,14 @@ constexpr int OS_KPT = 16;        // keys per thread
 constexpr int OS_TILE = OS_BLOCK * OS_KPT;  // 8192 keys per tile
 constexpr int HIST_BLOCK = 1024;
 
+// ---- persistent pipelined onesweep (8-bit digits) ----
+constexpr int OSP_BLOCK = 512;
+constexpr int OSP_KPT = 16;
+constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 8192 keys per tile
+constexpr int OSP_LBW = 4;                     // look-back window (predecessor tiles per round)
+constexpr int OSP_BLOCKS_PER_CU = 2;           // persistent grid = 2 x CUs (LDS ~59 KB, 127 VGPRs)
+static_assert(OSP_TILE == OS_TILE, "look-back layout shared with the 1-bit pass");
+
 // ---- LDS tile sort (merge path stage 1 / small sorts) ----
 constexpr int TS_BLOCK = 512;
 constexpr int TS_KPT = 16;
@@ -59,6 +67,8 @@ hipError_t launch_plan(const uint32_t *hist, size_t n, int bits, int in_is_out, 
 hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t n, uint32_t flip,
                            const uint32_t *hist, uint32_t *lookback, uint32_t *counter, uint32_t *err,
                            hipStream_t s);
+hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const uint32_t *hist,
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s);
 hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);

@@ -368,6 +368,214 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
 }
 
 // ---------------------------------------------------------------------------------
+// persistent, software-pipelined onesweep pass (8-bit digits)
+//
+// Measured on MI355X (harness/exp/onesweep_exp.hip): the non-persistent pass above
+// spends ~40 % of each tile waiting on the decoupled look-back, because the
+// inclusive-prefix chain advances only as fast as tiles finish their walks under
+// loaded memory latency.  Here each workgroup loops over dynamically acquired tiles
+// and keeps two in flight: tile A (already ranked and reordered, keys in
+// registers in scatter order) waits for its look-back while the workgroup loads,
+// histograms, publishes and ranks tile B.  Per tile:
+//   * the tile's digit histogram is built first (LDS atomics) and its aggregate
+//     published before ranking, so successors see it early;
+//   * the look-back reads a window of OSP_LBW predecessors per round;
+//   * the stable wave rank uses an LDS atomic-OR match (one 64-bit lane mask per
+//     digit and wave) instead of 8 ballots per key slot.
+// Dynamic tile ids (atomic counter) order the tiles by acquisition, so a tile only
+// ever waits on tiles whose aggregates are published unconditionally right after
+// their histogram: forward progress holds for any grid size or residency.
+// ---------------------------------------------------------------------------------
+struct OspSmem {
+    static constexpr int R = 256, W = OSP_BLOCK / WAVE, TILE = OSP_TILE;
+    uint32_t keys[TILE];
+    uint32_t wh[W * R];
+    uint64_t match[W * R];
+    uint32_t hist[R];
+    uint32_t gscan[R];
+    uint32_t delta[R];
+    uint32_t wsum[8];
+    uint32_t next;
+};
+
+__global__ __launch_bounds__(OSP_BLOCK) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
+                                                          uint32_t n, uint32_t flip,
+                                                          const uint32_t *__restrict__ ghist, uint32_t *lookback,
+                                                          uint32_t *counter, uint32_t *err) {
+    using S = OspSmem;
+    constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW;
+    static_assert(OSP_BLOCK == 512 && R <= OSP_BLOCK, "digit threads = waves 0-3");
+    __shared__ S sm;
+
+    const uint32_t srcsel = plan->src[pass];
+    if (srcsel == SEL_SKIP) return;  // every key has the same digit: identity pass
+    const uint32_t *__restrict__ in = bufs.p[srcsel];
+    uint32_t *__restrict__ out = bufs.p[plan->dst[pass]];
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t shift = (uint32_t)pass * 8u;
+    const uint32_t ntiles = (n + TILE - 1) / TILE;
+    const uint32_t sentinel = ~flip;  // digit 255 in every pass: ranks after all real keys
+
+    for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) {
+        sm.wh[i] = 0u;
+        sm.match[i] = 0ull;
+    }
+    const uint32_t gcount = tid < (uint32_t)R ? ghist[pass * R + tid] : 0u;
+    const uint32_t gex = block_excl_scan<OSP_BLOCK, R>(gcount, sm.wsum);
+    if (tid < (uint32_t)R) {
+        sm.gscan[tid] = gex;
+        sm.hist[tid] = 0u;
+    }
+    if (tid == 0) sm.next = atomicAdd(counter, 1u);
+    __syncthreads();
+    uint32_t tileB = sm.next;
+
+    // carried state of tile A
+    uint32_t tileA = 0xFFFFFFFFu, nvalidA = 0;
+    uint32_t kA[KPT];
+    uint32_t lwA[LBW];
+    uint32_t aggA = 0, dstartA = 0;
+    uint32_t *wh = sm.wh + wid * R;
+    uint64_t *wm = sm.match + wid * R;
+    for (;;) {
+        const bool haveB = tileB < ntiles;
+        const uint32_t baseB = tileB * (uint32_t)TILE;
+        const uint32_t nvalidB = haveB ? ((n - baseB) < (uint32_t)TILE ? (n - baseB) : (uint32_t)TILE) : 0u;
+        uint32_t kB[KPT], rB[KPT];
+        uint32_t hB = 0, xB = 0;
+        // look-back window of A (its latency hides behind B's load, histogram and rank)
+        if (tileA != 0xFFFFFFFFu && tid < (uint32_t)R) {
+            const int32_t hi = (int32_t)tileA - 1;
+#pragma unroll
+            for (int i = 0; i < LBW; ++i)
+                lwA[i] = (hi - i >= 0) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
+        }
+        if (haveB) {
+            const uint32_t wbase = baseB + wid * (KPT * WAVE) + lane;
+            if (nvalidB == (uint32_t)TILE) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) kB[j] = in[wbase + j * WAVE];
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
+            } else {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t idx = wbase + j * WAVE;
+                    kB[j] = idx < n ? in[idx] : sentinel;
+                    if (idx < n) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
+                }
+            }
+        }
+        __syncthreads();  // (1) histogram of B complete
+        if (haveB) {
+            if (tid < (uint32_t)R) {
+                hB = sm.hist[tid];
+                st_agent(lookback + (size_t)tileB * R + tid, (tileB == 0 ? LB_INC : LB_AGG) | hB);
+                xB = hB;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t t = __shfl_up(xB, off);
+                    if (lane >= (uint32_t)off) xB += t;
+                }
+                if (lane == 63) sm.wsum[wid] = xB;
+            }
+            // stable wave rank of B: lanes sharing a digit found by an LDS atomic-OR
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
+                uint64_t *slot = wm + d;
+                __hip_atomic_fetch_or(slot, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                const uint64_t m = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                const uint32_t pre = mbcnt64(m);
+                const uint32_t old = wh[d];
+                if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
+                rB[j] = ((old + pre) << 8) | d;
+            }
+        }
+        // complete the look-back of A; publish its inclusive prefix
+        if (tileA != 0xFFFFFFFFu && tid < (uint32_t)R) {
+            uint32_t excl = 0, spins = 0;
+            int32_t hi = (int32_t)tileA - 1;
+            for (;;) {
+                int consumed = 0;
+                bool done = false, stall = false;
+#pragma unroll
+                for (int i = 0; i < LBW; ++i) {
+                    if (!done && !stall) {
+                        if ((lwA[i] & ~LB_VAL) == 0u) stall = true;
+                        else {
+                            excl += lwA[i] & LB_VAL;
+                            ++consumed;
+                            done = (lwA[i] & LB_INC) != 0u;
+                        }
+                    }
+                }
+                if (done) break;
+                hi -= consumed;
+                if (stall) {
+                    if (++spins > SPIN_LIMIT) {
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+#pragma unroll
+                for (int i = 0; i < LBW; ++i)
+                    lwA[i] = (hi - i >= 0) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
+            }
+            if (tileA > 0) st_agent(lookback + (size_t)tileA * R + tid, LB_INC | (excl + aggA));
+            sm.delta[tid] = sm.gscan[tid] + excl - dstartA;
+        }
+        __syncthreads();  // (2) delta of A, wave counts and wsum of B
+        if (tileA != 0xFFFFFFFFu) {
+            if (nvalidA == (uint32_t)TILE) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
+                    out[sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i] = kA[j];
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
+                    if (i < nvalidA) out[sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i] = kA[j];
+                }
+            }
+        }
+        if (!haveB) break;
+        if (tid < (uint32_t)R) {
+            uint32_t add = 0;
+#pragma unroll
+            for (int w = 0; w < 4; ++w)
+                if ((uint32_t)w < wid) add += sm.wsum[w];
+            const uint32_t ds = xB + add - hB;  // tile-local start of digit tid
+            uint32_t run = ds;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t c = sm.wh[w * R + tid];
+                sm.wh[w * R + tid] = run;
+                run += c;
+            }
+            sm.hist[tid] = 0u;
+            dstartA = ds;
+        }
+        if (tid == 0) sm.next = atomicAdd(counter, 1u);
+        __syncthreads();  // (3) wave offsets of B
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) sm.keys[wh[rB[j] & 255u] + (rB[j] >> 8)] = kB[j];
+        __syncthreads();  // (4) B reordered in LDS
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[j * OSP_BLOCK + tid];
+        for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) sm.wh[i] = 0u;
+        tileA = tileB;
+        nvalidA = nvalidB;
+        aggA = hB;
+        tileB = sm.next;
+    }
+}
+
+// ---------------------------------------------------------------------------------
 // LDS-resident tile sort: 8-bit LSD passes entirely in LDS, one global read and write
 // ---------------------------------------------------------------------------------
 template <int BLOCK, int KPT>
@@ -667,6 +875,25 @@ hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t 
         k_onesweep<1, OS_BLOCK, OS_KPT><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback,
                                                                counter, err);
     else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+static int cu_count() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus;
+}
+
+hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const uint32_t *hist,
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s) {
+    const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE;
+    const size_t want = (size_t)OSP_BLOCKS_PER_CU * cu_count();
+    const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
+    k_onesweep_p<<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback, counter, err);
     return hipGetLastError();
 }
 
