@@ -75,10 +75,30 @@ class HipOps(Ops):
         return ((x & 0xFFFFFFFF) ^ f) <= ((y & 0xFFFFFFFF) ^ f)
 
 
-def _exchange(send: torch.Tensor, recv: torch.Tensor, partner: int, group=None) -> None:
-    ops = [dist.P2POp(dist.isend, send, partner, group=group), dist.P2POp(dist.irecv, recv, partner, group=group)]
-    for r in dist.batch_isend_irecv(ops):
-        r.wait()
+class P2PComm:
+    """Pairwise exchange over torch.distributed point-to-point ops (RCCL on the GPU
+    box: one xGMI link per pair; gloo on CPU)."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def exchange(self, send: torch.Tensor, recv: torch.Tensor, partner: int) -> None:
+        g = self.group
+        ops = [dist.P2POp(dist.isend, send, partner, group=g), dist.P2POp(dist.irecv, recv, partner, group=g)]
+        for r in dist.batch_isend_irecv(ops):
+            r.wait()
+
+
+class HostStagedComm(P2PComm):
+    """Test adapter: device tensors are staged through host memory and exchanged
+    with a CPU backend (gloo), so the GPU-side schedule (HipOps on one device) can
+    be exercised by several processes sharing one GPU."""
+
+    def exchange(self, send, recv, partner):
+        hs = send.cpu()
+        hr = torch.empty_like(hs)
+        super().exchange(hs, hr, partner)
+        recv.copy_(hr)
 
 
 def schedule(world: int):
@@ -94,7 +114,7 @@ def partner_and_side(rank: int, stage: int, step: int):
     return partner, keep_low
 
 
-def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, stride: int, group=None) -> int:
+def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, stride: int, comm) -> int:
     """Number k of keys that cross: the low side gives its top k, the high side its
     bottom k.  With L = low side's block and H = high side's block (both sorted, m
     keys), k = #H among the m smallest of L u H (L first on ties) = m - corank_L(m).
@@ -108,7 +128,7 @@ def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, str
     else:
         samp = mine[(m - 1) - idx]
     other = torch.empty_like(samp)
-    _exchange(samp.contiguous(), other, partner, group)
+    comm.exchange(samp.contiguous(), other, partner)
     Ls, Hs = (samp, other) if keep_low else (other, samp)
     Lh, Hh = Ls.cpu().tolist(), Hs.cpu().tolist()
     # first sample j with P(j*stride) false
@@ -124,7 +144,7 @@ def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, str
         else:
             win = mine[m - hi:m - lo].contiguous()
         owin = torch.empty_like(win)
-        _exchange(win, owin, partner, group)
+        comm.exchange(win, owin, partner)
         Lw, Hw = (win, owin) if keep_low else (owin, win)
         Lw, Hw = Lw.cpu().tolist(), Hw.cpu().tolist()
         # P(i) = L[i] <= H[m-1-i], i in [lo, hi): L[i] = Lw[i-lo], H[m-1-i] = Hw[(m-1-i)-(m-hi)] = Hw[hi-1-i]
@@ -137,12 +157,13 @@ def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, str
 
 
 def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, stride: int = 4096,
-              copy_input: bool = False) -> torch.Tensor:
+              copy_input: bool = False, comm=None) -> torch.Tensor:
     """Sort the global array whose rank-r shard is `local` (equal shard sizes).
     Returns this rank's shard of the sorted array (global ranks r*m .. r*m+m-1).
     `local` is sorted in place unless copy_input (then it is left untouched)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    comm = comm if comm is not None else P2PComm(group)
     if world & (world - 1):
         raise ValueError("dist_sort: world size must be a power of two")
     a = ops.local_sort(local, out_of_place=copy_input)
@@ -151,11 +172,11 @@ def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, s
         partner, keep_low = partner_and_side(rank, stage, step)
         if not partial:
             b = torch.empty_like(a)
-            _exchange(a.contiguous(), b, partner, group)
+            comm.exchange(a.contiguous(), b, partner)
             lo_blk, hi_blk = (a, b) if rank < partner else (b, a)  # same merge order on both sides
             a = ops.merge(lo_blk, hi_blk, 0, m) if keep_low else ops.merge(lo_blk, hi_blk, m, 2 * m)
             continue
-        k = _split_count(ops, a, partner, keep_low, stride, group)
+        k = _split_count(ops, a, partner, keep_low, stride, comm)
         if k == 0:
             continue
         if keep_low:
@@ -163,7 +184,7 @@ def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, s
         else:
             give = a[:k].contiguous()       # my bottom k go down
         got = torch.empty_like(give)
-        _exchange(give, got, partner, group)
+        comm.exchange(give, got, partner)
         if keep_low:
             a = ops.merge(a[:m - k], got, 0, m)   # keep my bottom m-k + partner's bottom k
         else:
