@@ -223,7 +223,7 @@ def main():
         traffic, tsrc = pmc_traffic(dom, n)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": traffic, "kernel": f"k_{dom}", "launches": k_cnt,
+                    "traffic": traffic, "kernel": ("k_onesweep_p" if dom == "onesweep" and args.algo == "radix" else f"k_{dom}"), "launches": k_cnt,
                     "avg_launch_ms": round(avg_ms, 5) if avg_ms else None,
                     "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
         cpu = None

@@ -11,6 +11,9 @@
 // its own device implementation of the same formula, and the tests check that
 // the two agree word for word.
 //
+// Pinning: parity unpinned by reference artifacts (the reference has no tests or
+// golden outputs and its CUDA source cannot be built here); see oracle/oracle.py.
+//
 // Build: oracle/Makefile -> oracle/liboracle.so (gcc, -fopenmp for the
 // __gnu_parallel baseline).
 #include <algorithm>

@@ -4,6 +4,15 @@ ctypes view of oracle/liboracle.so (std::sort spec oracle, the counter-based
 generator and the lane-level restatement of the reference's lab.cu).  Only
 tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this
 module; the product package never does.
+
+Pinning: parity unpinned by reference artifacts -- the reference ships no tests,
+golden vectors or validated outputs, and its lab.cu is CUDA-only (no nvcc here;
+a HIP build would need stand-in CUDA headers), so it cannot be run to produce
+any.  The oracle is pinned instead by (1) the uniqueness of a keys-only ascending
+sort (std::sort = the specification of order_array, letra.pdf p.3), checked
+against numpy's sort and the committed fixtures in tests/golden/, and (2) the
+lane-level restatement of lab.cu (labcu_restate.c), which reproduces the
+reference's own results, including its failure modes F4/F5/F6.
 """
 from __future__ import annotations
 
