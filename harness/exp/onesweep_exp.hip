@@ -583,7 +583,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_os6(const uint32_t *__restrict__
     if constexpr (SEGH) for (uint32_t i = tid; i < P * R; i += BLOCK) s_seg[i] = 0u;
     const uint32_t tps = ntiles / P;  // tiles per segment (P divides ntiles here)
     const uint32_t segshift = 31u - __builtin_clz(tps * TILE);  // tps * TILE is a power of two here
-    auto map = [&](uint32_t c) { return (c % P) * tps + c / P; };
+    const uint32_t tsh = 31u - __builtin_clz(tps);  // tps is a power of two in this experiment
+    auto map = [&](uint32_t c) { return ((c % P) << tsh) + c / P; };
     for (uint32_t i = tid; i < (uint32_t)(W * R); i += BLOCK) s_wh[i] = 0u;
     if constexpr (MT) for (uint32_t i = tid; i < (uint32_t)(W * R); i += BLOCK) s_match[i] = 0ull;
     if (tid < (uint32_t)R) s_hist[tid] = 0u;
@@ -627,7 +628,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_os6(const uint32_t *__restrict__
         if (haveB) {
             if (tid < (uint32_t)R) {
                 hB = s_hist[tid];
-                st_agent(lookback + (size_t)tileB * R + tid, (tileB % tps == 0 ? LB_INC : LB_AGG) | hB);
+                st_agent(lookback + (size_t)tileB * R + tid, ((tileB & (tps - 1)) == 0 ? LB_INC : LB_AGG) | hB);
                 xB = hB;
 #pragma unroll
                 for (int off = 1; off < 64; off <<= 1) {
@@ -701,8 +702,8 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_os6(const uint32_t *__restrict__
 #pragma unroll
                 for (int i = 0; i < LBW; ++i) lwA[i] = (hi - i >= loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
             }
-            if (!doneA && (tileA % tps)) st_agent(lookback + (size_t)tileA * R + tid, LB_INC | (excl + hA));
-            const uint32_t base = (P > 1) ? segoff[(size_t)(tileA / tps) * tps * R + tid] : gscan[tid];
+            if (!doneA && (tileA & (tps - 1))) st_agent(lookback + (size_t)tileA * R + tid, LB_INC | (excl + hA));
+            const uint32_t base = (P > 1) ? segoff[(size_t)((tileA >> tsh) << tsh) * R + tid] : gscan[tid];
             s_delta[tid] = base + excl - dstartA;
         }
         PH(3);
@@ -749,7 +750,7 @@ __global__ __launch_bounds__(BLOCK, OCC) void k_os6(const uint32_t *__restrict__
         hiA = (int32_t)tileB - 1;
         doneA = doneB;
         exclA = exclB;
-        loA = (int32_t)((tileB / tps) * tps);
+        loA = (int32_t)((tileB >> tsh) << tsh);
         tileB = s_next < ntiles ? map(s_next) : ntiles;
     }
     if constexpr (SEGH) {
@@ -1232,11 +1233,9 @@ int main() {
         CK(hipMemcpy(h0.data(), c.out, c.n * 4, hipMemcpyDeviceToHost));
         printf("v0 vs host stable counting sort: %s\n", memcmp(h0.data(), ref.data(), c.n * 4) ? "MISMATCH" : "match");
     }
-    run<512, 16, 4, 1, 16 << 16, 6>(c, "v8 = v6 + 16 segments", ref.data());
-    run<512, 16, 4, 0, 0, 9>(c, "v9 DMA prefetch, A in LDS", ref.data());
-    run<512, 16, 4, 0, 16 << 16, 9>(c, "v9 + 16 segments", ref.data());
-    run<512, 16, 8, 0, 16 << 16, 9>(c, "v9 W8 + 16 segments", ref.data());
-    run<256, 16, 4, 0, 16 << 16, 9>(c, "v9 + 16 segments", ref.data());
-    run<512, 12, 4, 0, 16 << 16, 9>(c, "v9 + 16 segments (partial)", nullptr);
+    run<512, 16, 4, 1, 0, 6>(c, "v6 (shift mapping)", ref.data());
+    run<512, 16, 4, 1, 16 << 16, 6>(c, "v8 16 segments (shift mapping)", ref.data());
+    run<512, 16, 4, 1, 64 << 16, 6>(c, "v8 64 segments (shift mapping)", ref.data());
+    run<512, 16, 8, 1, 16 << 16, 6>(c, "v8 W8 16 segments (shift mapping)", ref.data());
     return 0;
 }

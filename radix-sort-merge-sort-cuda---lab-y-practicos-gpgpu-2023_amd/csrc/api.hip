@@ -88,8 +88,9 @@ void timing_collect() {
 // ---------------------------------------------------------------------------------
 struct RadixLayout {
     int bits, R, P;
-    size_t ntiles;
-    size_t off_tmp, off_hist, off_counter, off_err, off_lookback, zero_bytes, off_plan, total;
+    size_t ntiles;  // look-back slots per pass (tiles + one partial tile per segment)
+    size_t off_tmp, off_hist, off_hps, off_joint, off_counter, off_err, off_lookback, zero_bytes, off_plan,
+        off_segplan, total;
 };
 
 RadixLayout radix_layout(size_t n, int bits) {
@@ -97,13 +98,17 @@ RadixLayout radix_layout(size_t n, int bits) {
     L.bits = bits;
     L.R = 1 << bits;
     L.P = (32 + bits - 1) / bits;
-    L.ntiles = (n + OS_TILE - 1) / OS_TILE;
+    L.ntiles = (n + OS_TILE - 1) / OS_TILE + (bits == 8 ? NSEG : 0);
     size_t o = 0;
     L.off_tmp = o;
     o = align_up(o + n * 4, 256);
-    // zeroed block: hist | counters | err | lookback (one memset per sort)
+    // zeroed block: hist | segment histograms | counters | err | lookback (one memset per sort)
     L.off_hist = o;
     o += (size_t)L.P * L.R * 4;
+    L.off_hps = o;
+    if (bits == 8) o += (size_t)NSEG * 4 * 256 * 4;
+    L.off_joint = o;
+    if (bits == 8) o += (size_t)4 * NSEG * 256 * 4;
     L.off_counter = o;
     o += (size_t)L.P * 4;
     L.off_err = o;
@@ -115,6 +120,8 @@ RadixLayout radix_layout(size_t n, int bits) {
     L.zero_bytes = o - L.off_hist;
     L.off_plan = o;
     o = align_up(o + sizeof(Plan), 256);
+    L.off_segplan = o;
+    if (bits == 8) o = align_up(o + 4 * sizeof(SegPlan), 256);
     L.total = o;
     return L;
 }
@@ -147,16 +154,32 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
     uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
     Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
     HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.zero_bytes, s));
-    {
-        TimingScope ts(LABSORT_K_HISTOGRAM, s);
-        HIP_TRY(launch_histogram(in, n, flip, bits, hist, s));
-    }
-    HIP_TRY(launch_plan(hist, n, bits, in == out ? 1 : 0, plan, s));
-    for (int p = 0; p < L.P; ++p) {
-        TimingScope ts(LABSORT_K_ONESWEEP, s);
-        uint32_t *lb = lookback + (size_t)p * L.ntiles * L.R;
-        if (bits == 8) HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, hist, lb, counters + p, err, s));
-        else HIP_TRY(launch_onesweep(b, plan, p, bits, n, flip, hist, lb, counters + p, err, s));
+    if (bits == 8) {
+        uint32_t *hps = reinterpret_cast<uint32_t *>(ws + L.off_hps);
+        uint32_t *joint = reinterpret_cast<uint32_t *>(ws + L.off_joint);
+        SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
+        {
+            TimingScope ts(LABSORT_K_HISTOGRAM, s);
+            HIP_TRY(launch_hist_seg(in, n, flip, hps, s));
+        }
+        HIP_TRY(launch_plan8(hps, n, in == out ? 1 : 0, plan, sps, hist, s));
+        for (int p = 0; p < L.P; ++p) {
+            if (p > 0) HIP_TRY(launch_segplan(plan, p, n, hist, joint, sps, s));
+            TimingScope ts(LABSORT_K_ONESWEEP, s);
+            HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
+                                      counters + p, err, joint, s));
+        }
+    } else {
+        {
+            TimingScope ts(LABSORT_K_HISTOGRAM, s);
+            HIP_TRY(launch_histogram(in, n, flip, bits, hist, s));
+        }
+        HIP_TRY(launch_plan(hist, n, bits, in == out ? 1 : 0, plan, s));
+        for (int p = 0; p < L.P; ++p) {
+            TimingScope ts(LABSORT_K_ONESWEEP, s);
+            HIP_TRY(launch_onesweep(b, plan, p, bits, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
+                                    counters + p, err, s));
+        }
     }
     HIP_TRY(launch_final_copy(b, plan, n, s));
     return LABSORT_OK;

@@ -23,6 +23,21 @@ constexpr int OSP_LBW = 4;                     // look-back window (predecessor 
 constexpr int OSP_BLOCKS_PER_CU = 2;           // persistent grid = 2 x CUs (LDS ~59 KB, 127 VGPRs)
 static_assert(OSP_TILE == OS_TILE, "look-back layout shared with the 1-bit pass");
 
+// ---- segmented look-back chains (8-bit radix) ----
+// Each pass's input is split into NSEG contiguous segments, each with its own
+// decoupled look-back chain; a segment's base offsets come from histograms the
+// upfront histogram kernel computes (see k_hist_seg / k_plan8).
+constexpr int NSEG = 16;
+constexpr int HS_BPS = 16;  // histogram workgroups per position segment
+struct SegPlan {
+    uint32_t start[NSEG + 1];  // segment s = pass input positions [start[s], start[s+1])
+    uint32_t tpre[NSEG + 1];   // tiles in segments < s = look-back slot of segment s's first tile
+    uint32_t maxt;             // most tiles in one segment
+    uint32_t mode;             // 0 position segments, 1 digit-group segments, 2 one segment
+    uint32_t pad[12];
+    uint32_t base[NSEG * 256];  // output offset of the first key of digit d in segment s
+};
+
 // ---- LDS tile sort (merge path stage 1 / small sorts) ----
 constexpr int TS_BLOCK = 512;
 constexpr int TS_KPT = 16;
@@ -35,6 +50,7 @@ constexpr int MG_TILE = MG_BLOCK * MG_KPT;  // 4096 outputs per workgroup
 
 constexpr int MAX_PASSES = 32;
 constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_SKIP = 0xFFu;
+constexpr uint32_t NEXT_NONE = 0xFFFFFFFFu;
 
 // Per-sort plan written on the device after the histogram (no host sync):
 // which buffer each digit pass reads and writes, or SKIP when every key has
@@ -43,6 +59,8 @@ constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_SKIP = 0xFFu;
 struct Plan {
     uint32_t src[MAX_PASSES];
     uint32_t dst[MAX_PASSES];
+    uint32_t next[MAX_PASSES];  // 8-bit radix: next active pass after this one (NEXT_NONE)
+    uint32_t prev[MAX_PASSES];  // 8-bit radix: previous active pass (NEXT_NONE for the first)
     uint32_t copy_from;  // SEL_SKIP: result already in OUT
     uint32_t active;     // number of non-trivial passes
     uint32_t pad[2];
@@ -67,8 +85,13 @@ hipError_t launch_plan(const uint32_t *hist, size_t n, int bits, int in_is_out, 
 hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t n, uint32_t flip,
                            const uint32_t *hist, uint32_t *lookback, uint32_t *counter, uint32_t *err,
                            hipStream_t s);
-hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const uint32_t *hist,
-                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s);
+hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, hipStream_t s);
+hipError_t launch_plan8(const uint32_t *hps, size_t n, int in_is_out, Plan *plan, SegPlan *segplans, uint32_t *hist,
+                        hipStream_t s);
+hipError_t launch_segplan(const Plan *plan, int pass, size_t n, const uint32_t *hist, const uint32_t *joint,
+                          SegPlan *segplans, hipStream_t s);
+hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, uint32_t *joint, hipStream_t s);
 hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);

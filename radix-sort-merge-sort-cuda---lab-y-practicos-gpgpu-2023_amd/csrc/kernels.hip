@@ -226,6 +226,211 @@ __global__ __launch_bounds__(256) void k_plan(const uint32_t *__restrict__ hist,
     plan->copy_from = (d[k - 1] == SEL_OUT) ? SEL_SKIP : d[k - 1];
 }
 
+// ---------------------------------------------------------------------------------
+// 8-bit radix front end and segment plans.
+//
+// Every pass runs NSEG independent decoupled look-back chains, one per contiguous
+// segment of its input; a segment's base offsets must therefore be known before
+// the pass starts:
+//   * first active pass: the input is split into NSEG equal position ranges and
+//     k_hist_seg (the upfront histogram, workgroups aligned to the ranges) gives
+//     each range's digit histograms: hps[s][p][d];
+//   * later passes: after a pass on digit p the data is ordered (stably) by digit
+//     p, so the keys whose digit p has top nibble g form one contiguous range of the
+//     next active pass's input.  The pass on digit p counts, per key, (top nibble of
+//     digit p, next active digit) into joint[q][g][d] as it histograms each tile,
+//     and k_segplan turns that into the next pass's segments and bases.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restrict__ keys, size_t n, uint32_t flip,
+                                                         uint32_t *__restrict__ hps) {
+    constexpr int SL = 32;  // replicated counters: the 32 lanes of a ds_add group hit 32 banks
+    __shared__ uint32_t h[4 * 256 * SL];
+    for (int i = threadIdx.x; i < 4 * 256 * SL; i += HIST_BLOCK) h[i] = 0u;
+    __syncthreads();
+    const uint32_t slot = threadIdx.x & (SL - 1);
+    auto count = [&](uint32_t k) {
+        k ^= flip;
+#pragma unroll
+        for (int p = 0; p < 4; ++p) atomicAdd(&h[(p * 256 + ((k >> (8 * p)) & 255u)) * SL + slot], 1u);
+    };
+    const uint32_t seg = blockIdx.x / HS_BPS, part = blockIdx.x % HS_BPS;
+    const size_t sb = (size_t)seg * n / NSEG, se = (size_t)(seg + 1) * n / NSEG;
+    const size_t per = (se - sb + HS_BPS - 1) / HS_BPS;
+    const size_t beg = sb + (size_t)part * per < se ? sb + (size_t)part * per : se;
+    const size_t end = beg + per < se ? beg + per : se;
+    if ((((uintptr_t)keys) & 15u) == 0) {
+        // scalar head up to 16-B alignment, uint4 body, scalar tail
+        const size_t abeg = (beg + 3) & ~(size_t)3;
+        const size_t vbeg = abeg < end ? abeg : end;
+        for (size_t t = beg + threadIdx.x; t < vbeg; t += HIST_BLOCK) count(keys[t]);
+        const size_t nv = (end - vbeg) / 4;
+        const uint4 *v = reinterpret_cast<const uint4 *>(keys + vbeg);
+        size_t i = threadIdx.x;
+        for (; i + 3 * HIST_BLOCK < nv; i += 4 * HIST_BLOCK) {
+            uint4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = v[i + u * HIST_BLOCK];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                count(x[u].x); count(x[u].y); count(x[u].z); count(x[u].w);
+            }
+        }
+        for (; i < nv; i += HIST_BLOCK) {
+            const uint4 x = v[i];
+            count(x.x); count(x.y); count(x.z); count(x.w);
+        }
+        for (size_t r = vbeg + nv * 4 + threadIdx.x; r < end; r += HIST_BLOCK) count(keys[r]);
+    } else {
+        for (size_t t = beg + threadIdx.x; t < end; t += HIST_BLOCK) count(keys[t]);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 4 * 256; i += HIST_BLOCK) {
+        uint32_t s = 0;
+#pragma unroll 8
+        for (int q = 0; q < SL; ++q) s += h[i * SL + ((q + i) & (SL - 1))];
+        if (s) atomicAdd(&hps[seg * 1024 + i], s);
+    }
+}
+
+// Writes SegPlan `sp` for a pass on digit q from per-segment digit-q histograms
+// hs[s][d] (s < NSEG) and segment starts.  256 threads (one per digit).
+__device__ void build_segplan(SegPlan *__restrict__ sp, const uint32_t *__restrict__ hs, const uint32_t *start,
+                              uint32_t mode, uint32_t *sh /* LDS: NSEG*256 + 8 words */) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
+    uint32_t tot = 0;
+    for (int s = 0; s < NSEG; ++s) {
+        const uint32_t v = hs[s * 256 + t];
+        sh[s * 256 + t] = v;
+        tot += v;
+    }
+    uint32_t x = tot;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    uint32_t *wsum = sh + NSEG * 256;
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t add = 0;
+    for (uint32_t w = 0; w < wid; ++w) add += wsum[w];
+    uint32_t run = x + add - tot;  // global start of digit t
+    for (int s = 0; s < NSEG; ++s) {
+        sp->base[s * 256 + t] = run;
+        run += sh[s * 256 + t];
+    }
+    if (t <= (uint32_t)NSEG) sp->start[t] = start[t];
+    if (t == 0) {
+        uint32_t tp = 0, mx = 0;
+        for (int s = 0; s <= NSEG; ++s) {
+            sp->tpre[s] = tp;
+            if (s < NSEG) {
+                const uint32_t ts = (start[s + 1] - start[s] + OSP_TILE - 1) / OSP_TILE;
+                tp += ts;
+                mx = ts > mx ? ts : mx;
+            }
+        }
+        sp->maxt = mx;
+        sp->mode = mode;
+    }
+}
+
+// Pass plan for the 8-bit radix (as k_plan: totals, trivial passes, ping-pong
+// buffers; plus each pass's next active digit) and the first active pass's SegPlan.
+__global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps, uint32_t n, int in_is_out,
+                                               Plan *__restrict__ plan, SegPlan *__restrict__ sps,
+                                               uint32_t *__restrict__ hist_out) {
+    __shared__ uint32_t hist[4 * 256];
+    __shared__ uint32_t sh[NSEG * 256 + 8];
+    __shared__ uint32_t triv[4];
+    __shared__ uint32_t start[NSEG + 1];
+    __shared__ int first;
+    const uint32_t t = threadIdx.x;
+    if (t < 4) triv[t] = 0;
+    __syncthreads();
+    uint32_t v[4] = {0, 0, 0, 0};
+    for (int s = 0; s < NSEG; ++s)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) v[p] += hps[s * 1024 + p * 256 + t];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        hist[p * 256 + t] = v[p];
+        hist_out[p * 256 + t] = v[p];
+        if (v[p] == n) triv[p] = 1;
+    }
+    if (t <= (uint32_t)NSEG) start[t] = (uint32_t)((size_t)t * n / NSEG);
+    __syncthreads();
+    if (t == 0) {
+        int act[4];
+        int k = 0;
+        for (int p = 0; p < MAX_PASSES; ++p) {
+            plan->src[p] = SEL_SKIP;
+            plan->dst[p] = SEL_SKIP;
+            plan->next[p] = NEXT_NONE;
+        }
+        for (int p = 0; p < 4; ++p)
+            if (!triv[p]) act[k++] = p;
+        for (int i = 0; i + 1 < k; ++i) plan->next[act[i]] = (uint32_t)act[i + 1];
+        plan->active = (uint32_t)k;
+        first = k ? act[0] : -1;
+        if (k == 0) {
+            plan->copy_from = in_is_out ? SEL_SKIP : SEL_IN;
+        } else {
+            uint32_t d[4];
+            uint32_t cur = SEL_OUT;
+            for (int i = k - 1; i >= 0; --i) {
+                d[i] = cur;
+                cur = (cur == SEL_OUT) ? SEL_TMP : SEL_OUT;
+            }
+            if (in_is_out && d[0] == SEL_OUT)
+                for (int i = 0; i < k; ++i) d[i] = (i & 1) ? SEL_OUT : SEL_TMP;
+            uint32_t src = SEL_IN;
+            for (int i = 0; i < k; ++i) {
+                plan->src[act[i]] = src;
+                plan->dst[act[i]] = d[i];
+                plan->prev[act[i]] = i ? (uint32_t)act[i - 1] : NEXT_NONE;
+                src = d[i];
+            }
+            plan->copy_from = (d[k - 1] == SEL_OUT) ? SEL_SKIP : d[k - 1];
+        }
+    }
+    __syncthreads();
+    if (first < 0) return;
+    // first active pass: position segments; hs[s][d] = hps[s][first][d]
+    for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = hps[s * 1024 + first * 256 + t];
+    __syncthreads();
+    build_segplan(sps + first, sh, start, 0u, sh);
+}
+
+// SegPlan of pass q when q is active and not the first: segments = ranges of the
+// previous active digit's top nibble (starts from its histogram), histograms from
+// the joint counts the previous pass wrote.
+__global__ __launch_bounds__(256) void k_segplan(const Plan *__restrict__ plan, int q, uint32_t n,
+                                                 const uint32_t *__restrict__ hist, const uint32_t *__restrict__ joint,
+                                                 SegPlan *__restrict__ sps) {
+    __shared__ uint32_t sh[NSEG * 256 + 8];
+    __shared__ uint32_t start[NSEG + 1];
+    const uint32_t prev = plan->prev[q];
+    if (plan->src[q] == SEL_SKIP || prev == NEXT_NONE) return;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
+    // segment starts: exclusive prefix over nibble groups of hist[prev]
+    const uint32_t v = hist[prev * 256 + t];
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    if (lane == 63) sh[NSEG * 256 + wid] = x;
+    __syncthreads();
+    uint32_t add = 0;
+    for (uint32_t w = 0; w < wid; ++w) add += sh[NSEG * 256 + w];
+    if ((t & 15u) == 0) start[t >> 4] = x + add - v;
+    if (t == 0) start[NSEG] = n;
+    __syncthreads();
+    build_segplan(sps + q, joint + (size_t)q * NSEG * 256, start, 1u, sh);
+}
+
 __global__ __launch_bounds__(256) void k_final_copy(Bufs b, const Plan *__restrict__ plan, size_t n) {
     const uint32_t from = plan->copy_from;
     if (from == SEL_SKIP) return;
@@ -392,19 +597,23 @@ struct OspSmem {
     uint32_t wh[W * R];
     uint64_t match[W * R];
     uint32_t hist[R];
-    uint32_t gscan[R];
     uint32_t delta[R];
+    uint32_t start[NSEG + 1];
+    uint32_t tpre[NSEG + 1];
+    uint32_t joint[NSEG * R];  // (top nibble of this digit, next active digit) counts
     uint32_t wsum[8];
     uint32_t next;
 };
 
-__global__ __launch_bounds__(OSP_BLOCK) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
-                                                          uint32_t n, uint32_t flip,
-                                                          const uint32_t *__restrict__ ghist, uint32_t *lookback,
-                                                          uint32_t *counter, uint32_t *err) {
+constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(OSP_BLOCK, 2 * OSP_BLOCK / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
+                                                          uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
+                                                          uint32_t *lookback, uint32_t *counter, uint32_t *err,
+                                                          uint32_t *__restrict__ joint) {
     using S = OspSmem;
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW;
-    static_assert(OSP_BLOCK == 512 && R <= OSP_BLOCK, "digit threads = waves 0-3");
+    static_assert(OSP_BLOCK == 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
     __shared__ S sm;
 
     const uint32_t srcsel = plan->src[pass];
@@ -413,56 +622,73 @@ __global__ __launch_bounds__(OSP_BLOCK) void k_onesweep_p(Bufs bufs, const Plan 
     uint32_t *__restrict__ out = bufs.p[plan->dst[pass]];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t shift = (uint32_t)pass * 8u;
-    const uint32_t ntiles = (n + TILE - 1) / TILE;
     const uint32_t sentinel = ~flip;  // digit 255 in every pass: ranks after all real keys
+    const uint32_t climit = NSEG * sp->maxt;
+    const uint32_t nxt = plan->next[pass];
+    const bool count_next = nxt != NEXT_NONE;
+    const uint32_t nshift = count_next ? nxt * 8u : 0u;
 
     for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) {
         sm.wh[i] = 0u;
         sm.match[i] = 0ull;
     }
-    const uint32_t gcount = tid < (uint32_t)R ? ghist[pass * R + tid] : 0u;
-    const uint32_t gex = block_excl_scan<OSP_BLOCK, R>(gcount, sm.wsum);
-    if (tid < (uint32_t)R) {
-        sm.gscan[tid] = gex;
-        sm.hist[tid] = 0u;
+    for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += OSP_BLOCK) sm.joint[i] = 0u;
+    if (tid <= (uint32_t)NSEG) {
+        sm.start[tid] = sp->start[tid];
+        sm.tpre[tid] = sp->tpre[tid];
     }
-    if (tid == 0) sm.next = atomicAdd(counter, 1u);
+    if (tid < (uint32_t)R) sm.hist[tid] = 0u;
+    // tile acquisition: c -> segment c & 15, tile c >> 4 of that segment; ids past a
+    // segment's last tile are skipped, so every segment's tiles are acquired in order
+    auto acquire = [&]() {
+        for (;;) {
+            const uint32_t c = atomicAdd(counter, 1u);
+            if (c >= climit) return OSP_DONE;
+            const uint32_t sg = c & (NSEG - 1), l = c >> 4;
+            if (l < sp->tpre[sg + 1] - sp->tpre[sg]) return c;
+        }
+    };
+    if (tid == 0) sm.next = acquire();
     __syncthreads();
-    uint32_t tileB = sm.next;
+    uint32_t cB = sm.next;
 
-    // carried state of tile A
-    uint32_t tileA = 0xFFFFFFFFu, nvalidA = 0;
+    // carried state of tile A (slot = look-back slot, lo = slot of its segment's first tile)
+    uint32_t slotA = OSP_DONE, loA = 0, segA = 0, nvalidA = 0;
     uint32_t kA[KPT];
     uint32_t lwA[LBW];
     uint32_t aggA = 0, dstartA = 0;
     uint32_t *wh = sm.wh + wid * R;
     uint64_t *wm = sm.match + wid * R;
     for (;;) {
-        const bool haveB = tileB < ntiles;
-        const uint32_t baseB = tileB * (uint32_t)TILE;
-        const uint32_t nvalidB = haveB ? ((n - baseB) < (uint32_t)TILE ? (n - baseB) : (uint32_t)TILE) : 0u;
+        const bool haveB = cB != OSP_DONE;
+        const uint32_t segB = cB & (NSEG - 1), lB = cB >> 4;
+        const uint32_t loB = haveB ? sm.tpre[segB] : 0u, slotB = loB + lB;
+        const uint32_t begB = haveB ? sm.start[segB] + lB * (uint32_t)TILE : 0u;
+        const uint32_t endB = haveB ? sm.start[segB + 1] : 0u;
+        const uint32_t nvalidB = (endB - begB) < (uint32_t)TILE ? (endB - begB) : (uint32_t)TILE;
         uint32_t kB[KPT], rB[KPT];
         uint32_t hB = 0, xB = 0;
         // look-back window of A (its latency hides behind B's load, histogram and rank)
-        if (tileA != 0xFFFFFFFFu && tid < (uint32_t)R) {
-            const int32_t hi = (int32_t)tileA - 1;
+        if (slotA != OSP_DONE && tid < (uint32_t)R) {
+            const int32_t hi = (int32_t)slotA - 1;
 #pragma unroll
             for (int i = 0; i < LBW; ++i)
-                lwA[i] = (hi - i >= 0) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
+                lwA[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
         }
         if (haveB) {
-            const uint32_t wbase = baseB + wid * (KPT * WAVE) + lane;
+            const uint32_t woff = wid * (KPT * WAVE) + lane;
+            const uint32_t *src = in + begB + woff;
             if (nvalidB == (uint32_t)TILE) {
 #pragma unroll
-                for (int j = 0; j < KPT; ++j) kB[j] = in[wbase + j * WAVE];
+                for (int j = 0; j < KPT; ++j) kB[j] = src[j * WAVE];
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
             } else {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
-                    const uint32_t idx = wbase + j * WAVE;
-                    kB[j] = idx < n ? in[idx] : sentinel;
-                    if (idx < n) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
+                    const bool ok = woff + j * WAVE < nvalidB;
+                    kB[j] = ok ? src[j * WAVE] : sentinel;
+                    if (ok) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
                 }
             }
         }
@@ -470,7 +696,7 @@ __global__ __launch_bounds__(OSP_BLOCK) void k_onesweep_p(Bufs bufs, const Plan 
         if (haveB) {
             if (tid < (uint32_t)R) {
                 hB = sm.hist[tid];
-                st_agent(lookback + (size_t)tileB * R + tid, (tileB == 0 ? LB_INC : LB_AGG) | hB);
+                st_agent(lookback + (size_t)slotB * R + tid, (lB == 0 ? LB_INC : LB_AGG) | hB);
                 xB = hB;
 #pragma unroll
                 for (int off = 1; off < 64; off <<= 1) {
@@ -493,10 +719,10 @@ __global__ __launch_bounds__(OSP_BLOCK) void k_onesweep_p(Bufs bufs, const Plan 
                 rB[j] = ((old + pre) << 8) | d;
             }
         }
-        // complete the look-back of A; publish its inclusive prefix
-        if (tileA != 0xFFFFFFFFu && tid < (uint32_t)R) {
+        // complete the look-back of A; publish its inclusive prefix (within its segment)
+        if (slotA != OSP_DONE && tid < (uint32_t)R) {
             uint32_t excl = 0, spins = 0;
-            int32_t hi = (int32_t)tileA - 1;
+            int32_t hi = (int32_t)slotA - 1;
             for (;;) {
                 int consumed = 0;
                 bool done = false, stall = false;
@@ -522,13 +748,13 @@ __global__ __launch_bounds__(OSP_BLOCK) void k_onesweep_p(Bufs bufs, const Plan 
                 }
 #pragma unroll
                 for (int i = 0; i < LBW; ++i)
-                    lwA[i] = (hi - i >= 0) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
+                    lwA[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
             }
-            if (tileA > 0) st_agent(lookback + (size_t)tileA * R + tid, LB_INC | (excl + aggA));
-            sm.delta[tid] = sm.gscan[tid] + excl - dstartA;
+            if (slotA > loA) st_agent(lookback + (size_t)slotA * R + tid, LB_INC | (excl + aggA));
+            sm.delta[tid] = sp->base[segA * R + tid] + excl - dstartA;
         }
         __syncthreads();  // (2) delta of A, wave counts and wsum of B
-        if (tileA != 0xFFFFFFFFu) {
+        if (slotA != OSP_DONE) {
             if (nvalidA == (uint32_t)TILE) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
@@ -560,7 +786,7 @@ __global__ __launch_bounds__(OSP_BLOCK) void k_onesweep_p(Bufs bufs, const Plan 
             sm.hist[tid] = 0u;
             dstartA = ds;
         }
-        if (tid == 0) sm.next = atomicAdd(counter, 1u);
+        if (tid == 0) sm.next = acquire();
         __syncthreads();  // (3) wave offsets of B
 #pragma unroll
         for (int j = 0; j < KPT; ++j) sm.keys[wh[rB[j] & 255u] + (rB[j] >> 8)] = kB[j];
@@ -568,10 +794,26 @@ __global__ __launch_bounds__(OSP_BLOCK) void k_onesweep_p(Bufs bufs, const Plan 
 #pragma unroll
         for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[j * OSP_BLOCK + tid];
         for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) sm.wh[i] = 0u;
-        tileA = tileB;
+        if (count_next) {  // (top nibble of this digit, next active digit) of B's valid keys
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t x = kA[j] ^ flip;
+                if ((uint32_t)j * OSP_BLOCK + tid < nvalidB)
+                    atomicAdd(&sm.joint[((x >> (shift + 4)) & 15u) * R + ((x >> nshift) & 255u)], 1u);
+            }
+        }
+        slotA = slotB;
+        loA = loB;
+        segA = segB;
         nvalidA = nvalidB;
         aggA = hB;
-        tileB = sm.next;
+        cB = sm.next;
+    }
+    if (count_next) {
+        __syncthreads();
+        uint32_t *j = joint + (size_t)nxt * NSEG * R;
+        for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += OSP_BLOCK)
+            if (sm.joint[i]) atomicAdd(&j[i], sm.joint[i]);
     }
 }
 
@@ -888,12 +1130,30 @@ static int cu_count() {
     return cus;
 }
 
-hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const uint32_t *hist,
-                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s) {
-    const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE;
+hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, uint32_t *joint, hipStream_t s) {
+    const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE + NSEG;
     const size_t want = (size_t)OSP_BLOCKS_PER_CU * cu_count();
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
-    k_onesweep_p<<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback, counter, err);
+    k_onesweep_p<<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint);
+    return hipGetLastError();
+}
+
+hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    k_hist_seg<<<NSEG * HS_BPS, HIST_BLOCK, 0, s>>>(keys, n, flip, hps);
+    return hipGetLastError();
+}
+
+hipError_t launch_plan8(const uint32_t *hps, size_t n, int in_is_out, Plan *plan, SegPlan *segplans, uint32_t *hist,
+                        hipStream_t s) {
+    k_plan8<<<1, 256, 0, s>>>(hps, (uint32_t)n, in_is_out, plan, segplans, hist);
+    return hipGetLastError();
+}
+
+hipError_t launch_segplan(const Plan *plan, int pass, size_t n, const uint32_t *hist, const uint32_t *joint,
+                          SegPlan *segplans, hipStream_t s) {
+    k_segplan<<<1, 256, 0, s>>>(plan, pass, (uint32_t)n, hist, joint, segplans);
     return hipGetLastError();
 }
 

@@ -237,3 +237,35 @@ def test_timing_hooks(ls, oracle, torch_gpu):
     ms, cnt = ls.timing_read("onesweep")
     ls.timing_enable(False)
     assert cnt == 4 and ms > 0
+
+
+# ---- segmented look-back chains: pass structure edge cases ----------------------------
+@pytest.mark.parametrize("mask,name", [
+    (0xFFFF00FF, "trivial middle pass (byte 1 constant)"),
+    (0x0F0F0F0F, "every digit in nibble group 0 (one segment holds all keys)"),
+    (0xFF0000FF, "two trivial middle passes"),
+    (0xF0F0F0F0, "every digit's low nibble zero"),
+    (0x000000FF, "one active pass"),
+    (0x80000001, "sign bit + bit 0 only"),
+])
+@pytest.mark.parametrize("key", ["u32", "i32"])
+@pytest.mark.parametrize("n", [8192 * 16 + 5, (1 << 21) + 777])
+def test_sort_device_pass_structure(ls, oracle, torch_gpu, mask, name, key, n):
+    torch = torch_gpu
+    a = oracle.gen(n, SEED + 16, "u32") & np.uint32(mask)
+    t = to_dev(torch, a)
+    o = torch.empty_like(t)
+    ls.sort_device(t, o, n, key=key, algo="radix")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key), err_msg=name)
+
+
+@pytest.mark.parametrize("n", [1, 100, 8191, 8193, 16 * 8192 - 1, 16 * 8192 + 1, 3 * 16 * 8192 + 4097])
+def test_sort_device_segment_boundaries(ls, oracle, torch_gpu, n):
+    """Sizes around the 16 position segments x 8192-key tiles of the first pass."""
+    torch = torch_gpu
+    a = oracle.gen(n, SEED + 17 + n, "u32")
+    t = to_dev(torch, a)
+    ls.sort_device(t, t, n, algo="radix")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(from_dev(t), oracle.sort_u32(a))
