@@ -52,6 +52,10 @@ def parse():
     ap.add_argument("--dist", default="u32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--exchange", default="splitters", choices=["splitters", "pairwise"],
+                    help="N>1: all-peer splitter exchange + merge tree, or the bitonic pairwise merge-split network")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N>1 only; gloo (+ host-staged exchange) is a test mode for several ranks on one GPU")
     return ap.parse_args()
 
 
@@ -121,8 +125,10 @@ def main():
     if world != args.gpus:
         if args.gpus > 1 and world == 1:
             sys.exit("bench.py: --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+    local = local % max(torch.cuda.device_count(), 1)  # ranks share a device only in the gloo test mode
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # where collectives' tensors live
     if REPO not in sys.path:
         sys.path.insert(0, REPO)
     ls = importlib.import_module(PKG_NAME)
@@ -134,8 +140,12 @@ def main():
 
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
         dmod = importlib.import_module(PKG_NAME + ".dist")
+        comm = dmod.P2PComm() if args.backend == "nccl" else dmod.HostStagedComm()
         ops = dmod.HipOps(ls, key=key, local_algo="radix", stream=stream)
         src = torch.empty(n, dtype=torch.int32, device=dev)
         with torch.cuda.stream(stream):
@@ -143,7 +153,9 @@ def main():
 
         def step():
             with torch.cuda.stream(stream):
-                return dmod.dist_sort(src, ops, copy_input=True)
+                if args.exchange == "splitters":
+                    return dmod.dist_sort_splitters(src, ops, copy_input=True, comm=comm)
+                return dmod.dist_sort(src, ops, copy_input=True, comm=comm)
 
         def barrier():
             dist.barrier()
@@ -181,28 +193,37 @@ def main():
 
     if world > 1:
         import torch.distributed as dist
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
         # global check: every shard sorted, boundaries ordered, multiset preserved
+        nres = res.numel()  # the splitter exchange leaves ranges of slightly different sizes
         cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-        ls.count_descents(res, n, cnt, key=key)
-        edges = torch.stack([res[0], res[-1]]).to(torch.int64) & 0xFFFFFFFF
+        ls.count_descents(res, nres, cnt, key=key)
+        f = 0x80000000 if key == "i32" else 0
+        edges = ((torch.stack([res[0], res[-1]]).to(torch.int64) & 0xFFFFFFFF) ^ f).to(cdev) if nres else \
+            torch.tensor([2**33, -1], dtype=torch.int64, device=cdev)  # empty range: neutral for the order check
         allg = [torch.empty_like(edges) for _ in range(world)]
         dist.all_gather(allg, edges)
         h_in = torch.zeros(1024, dtype=torch.int32, device=dev)
         h_out = torch.zeros(1024, dtype=torch.int32, device=dev)
         ls.histogram(src, n, h_in, key=key)
-        ls.histogram(res, n, h_out, key=key)
+        ls.histogram(res, nres, h_out, key=key)
         s_in = (src.to(torch.int64) & 0xFFFFFFFF).sum()
         s_out = (res.to(torch.int64) & 0xFFFFFFFF).sum()
-        red = torch.stack([s_in, s_out])
+        red = torch.stack([s_in, s_out]).to(cdev)
+        h_in, h_out = h_in.to(cdev), h_out.to(cdev)
         dist.all_reduce(h_in)
         dist.all_reduce(h_out)
         dist.all_reduce(red)
         ok = int(cnt.item()) == 0 and torch.equal(h_in, h_out) and int(red[0]) == int(red[1])
-        ok = ok and all(int(allg[i][1]) <= int(allg[i + 1][0]) for i in range(world - 1))
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+        lastmax = -1
+        for e in allg:  # ranges in rank order: each range's first key >= every earlier key
+            if int(e[0]) > 2**32:
+                continue
+            ok = ok and int(e[0]) >= lastmax
+            lastmax = int(e[1])
+        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
         dist.all_reduce(okt, op=dist.ReduceOp.MIN)
         ok = bool(okt.item())
     else:
@@ -232,8 +253,10 @@ def main():
         wl = {"radix": "LSD radix sort (8-bit digits, onesweep)", "merge": "LDS tile sort + merge-path passes",
               "radix1": "LSD radix with 1-bit split passes (letra.pdf)"}[args.algo]
         if world > 1:
+            how = ("splitter exchange (pairwise send/recv to all peers at once) + merge tree"
+                   if args.exchange == "splitters" else "bitonic pairwise merge-split network")
             workload = (f"merge sort across {world} GPUs: local radix sort of 2^{args.log2n} uint32 keys per GPU "
-                        f"+ pairwise merge-split over RCCL (BASELINE config 5 shape, weak scaling)")
+                        f"+ {how} over RCCL/xGMI (BASELINE config 5 shape, weak scaling)")
         else:
             workload = f"{wl}, n=2^{args.log2n} uint32 {args.dist}, device-resident (BASELINE config 3)"
         line = {
@@ -244,7 +267,7 @@ def main():
             "data": "synthetic (counter-based splitmix64 generator on device)",
             "config": {"workload": workload, "n_per_gpu": n, "algo": args.algo if world == 1 else "merge",
                        "key": key, "dist": args.dist,
-                       "parallelism": "single GPU" if world == 1 else f"{world} ranks, RCCL pairwise merge-split"},
+                       "parallelism": "single GPU" if world == 1 else f"{world} ranks, RCCL {args.exchange} exchange"},
             "verified": "sorted permutation (descents, digit histograms, sums)",
             "roofline": roofline, "cpu_baseline": cpu,
         }

@@ -36,3 +36,10 @@ if [[ "$STEPS" == all || "$STEPS" == *prof* ]]; then
   done
 fi
 run done
+if [[ "$STEPS" == *dist* ]]; then
+  for ex in splitters pairwise; do
+    run "bench gloo 2 ranks on one GPU ($ex)"
+    timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 "$R/bench.py" --gpus 2 --steps 3 --warmup 1 --backend gloo --log2n 22 --exchange $ex > "$O/bench_dist2_$ex.log" 2>&1 || { tail -30 "$O/bench_dist2_$ex.log"; exit 1; }
+    grep '"metric"' "$O/bench_dist2_$ex.log" | cut -c1-400
+  done
+fi

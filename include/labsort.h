@@ -105,6 +105,12 @@ int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *
  * (p = 0 .. ceil(32/bits)-1); bits = 8 or 1.  d_hist must be zeroed by the caller. */
 int labsort_histogram(const void *d_keys, size_t n, int key_type, int bits, uint32_t *d_hist, void *stream);
 
+/* d_out[i] = number of keys <= d_values[i] in the sorted run d_sorted[0..n) (key order):
+ * the cut points of a rank's sorted shard at the common splitters of the multi-GPU
+ * exchange (no lab.cu counterpart: the reference is single-GPU). */
+int labsort_upper_bound(const void *d_sorted, size_t n, int key_type, const uint32_t *d_values, size_t nv,
+                        uint32_t *d_out, void *stream);
+
 /* ---- utilities ---- */
 /* Counter-based generator, identical to oracle_fill: keys first..first+n-1. */
 int labsort_fill(void *d_out, size_t n, uint64_t seed, int dist, uint64_t param, uint64_t first, void *stream);

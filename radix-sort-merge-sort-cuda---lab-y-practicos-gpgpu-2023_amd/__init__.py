@@ -37,7 +37,7 @@ C_SYMBOLS = [
     "labsort_max_keys", "labsort_tile_keys", "labsort_merge_tile_keys", "labsort_workspace_bytes",
     "labsort_sort_device", "labsort_sort_host", "labsort_wave_tile_sort", "labsort_tile_sort",
     "labsort_merge_parts", "labsort_merge_pass", "labsort_merge", "labsort_histogram", "labsort_fill",
-    "labsort_count_descents", "labsort_timing_enable", "labsort_timing_read", "sort",
+    "labsort_count_descents", "labsort_timing_enable", "labsort_timing_read", "labsort_upper_bound", "sort",
 ]
 CXX_SYMBOLS = ["_Z11order_arrayPii", "_Z16order_with_trustPii"]
 
@@ -84,6 +84,7 @@ def _load() -> ctypes.CDLL:
     L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
     L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
     L.labsort_count_descents.argtypes = [p, sz, i, p, p]
+    L.labsort_upper_bound.argtypes = [p, sz, i, p, sz, p, p]
     L.labsort_timing_enable.argtypes = [i]
     L.labsort_timing_read.argtypes = [i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
     L.sort.argtypes = [p, i]
@@ -223,6 +224,12 @@ def fill(d_out, n: int, seed: int, dist: str = "u32", param: int = 0, first: int
         param = first + n
     _check(lib.labsort_fill(_ptr(d_out), n, seed & (2**64 - 1), DIST[dist], param, first, _stream(stream)),
            "fill")
+
+
+def upper_bound(d_sorted, n: int, d_values, nv: int, d_out, key: str = "u32", stream=None) -> None:
+    """d_out[i] = number of keys <= d_values[i] in the sorted run (key order)."""
+    _check(lib.labsort_upper_bound(_ptr(d_sorted) if n else 0, n, KEY[key], _ptr(d_values), nv, _ptr(d_out),
+                                   _stream(stream)), "upper_bound")
 
 
 def count_descents(d_keys, n: int, d_count, key: str = "u32", stream=None) -> None:

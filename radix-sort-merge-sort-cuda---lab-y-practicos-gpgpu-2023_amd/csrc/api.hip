@@ -393,6 +393,16 @@ int labsort_fill(void *d_out, size_t n, uint64_t seed, int dist, uint64_t param,
     return LABSORT_OK;
 }
 
+int labsort_upper_bound(const void *d_sorted, size_t n, int key_type, const uint32_t *d_values, size_t nv,
+                        uint32_t *d_out, void *stream) {
+    if (nv == 0) return LABSORT_OK;
+    if (!d_values || !d_out || (n && !d_sorted) || n > 0xFFFFFFFFu) return LABSORT_ERR_ARG;
+    if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
+    HIP_TRY(launch_upper_bound(static_cast<const uint32_t *>(d_sorted), n, flip_of(key_type), d_values, nv, d_out,
+                               as_stream(stream)));
+    return LABSORT_OK;
+}
+
 int labsort_count_descents(const void *d_keys, size_t n, int key_type, uint32_t *d_count, void *stream) {
     if (n < 2) return LABSORT_OK;
     if (!d_keys || !d_count) return LABSORT_ERR_ARG;

@@ -99,6 +99,8 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
                              uint32_t *part, hipStream_t s);
 hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size_t lb, uint32_t *out, size_t d0,
                            size_t d1, uint32_t flip, uint32_t *part, hipStream_t s);
+hipError_t launch_upper_bound(const uint32_t *keys, size_t n, uint32_t flip, const uint32_t *values, size_t nv,
+                              uint32_t *out, hipStream_t s);
 hipError_t launch_count_descents(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *count, hipStream_t s);
 
 }  // namespace labsort

@@ -1074,6 +1074,26 @@ __global__ __launch_bounds__(256) void k_count_descents(const uint32_t *__restri
     }
 }
 
+// ---------------------------------------------------------------------------------
+// splitter partition of a sorted run: out[i] = number of keys <= values[i]
+// (upper bound, key order), one thread per value -- the multi-GPU exchange cuts
+// each rank's sorted shard at the common splitters with it.
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_upper_bound(const uint32_t *__restrict__ keys, uint32_t n, uint32_t flip,
+                                                    const uint32_t *__restrict__ values, uint32_t nv,
+                                                    uint32_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nv) return;
+    const uint32_t v = values[i] ^ flip;
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if ((keys[mid] ^ flip) <= v) lo = mid + 1;
+        else hi = mid;
+    }
+    out[i] = lo;
+}
+
 // =================================================================================
 // host launchers
 // =================================================================================
@@ -1196,6 +1216,13 @@ hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     k_merge_ab<MG_BLOCK, MG_KPT><<<ntiles, MG_BLOCK, 0, s>>>(a, b, out, (uint32_t)d0, (uint32_t)d1, flip, part);
+    return hipGetLastError();
+}
+
+hipError_t launch_upper_bound(const uint32_t *keys, size_t n, uint32_t flip, const uint32_t *values, size_t nv,
+                              uint32_t *out, hipStream_t s) {
+    if (nv == 0) return hipSuccess;
+    k_upper_bound<<<(unsigned)((nv + 63) / 64), 64, 0, s>>>(keys, (uint32_t)n, flip, values, (uint32_t)nv, out);
     return hipGetLastError();
 }
 

@@ -1,4 +1,4 @@
-"""Multi-GPU merge sort: one process per GPU, pairwise merge-split over RCCL/xGMI.
+"""Multi-GPU merge sort: one process per GPU, pairwise RCCL send/recv over xGMI.
 
 The reference runs on one GPU only (run.sh:11); the north_star partitions n over
 the GPUs of one node for the merge-sort path: every rank sorts its shard locally,
@@ -15,9 +15,21 @@ steps for p ranks.  `partial=True` moves only the keys that cross: both sides
 first swap a strided sample of their shards, bracket the split point, swap the
 bracketing window, agree on the exact split k, then send k keys each way.
 
+`dist_sort_splitters` is the all-link form (the default of bench.py): every rank
+sorts its shard, the ranks agree on p-1 splitters from a regular sample of every
+shard (one all_gather), cut their sorted shards at the splitters
+(`labsort_upper_bound`), send piece j to rank j with pairwise send/recv posted to
+all peers at once (so all 7 xGMI links of a node carry data together instead of
+one per step), and merge the p received runs in rank order with a merge tree
+(`labsort_merge`, A before B on ties).  Rank r then holds the r-th contiguous
+range of the sorted array; range sizes follow the splitters (within a few percent
+of n/p on varied data; skewed data with a heavy repeated key can unbalance them).
+
 Local operations are pluggable (`Ops`): the product uses liblabsort.so on the
 rank's GPU (`HipOps`); the CPU tests inject an oracle-backed implementation so the
 exchange schedule is exercised with the gloo backend on machines without GPUs.
+Communication is pluggable too (`P2PComm` = torch.distributed; `HostStagedComm`
+stages device tensors through host memory for a CPU backend in tests).
 """
 from __future__ import annotations
 
@@ -40,6 +52,15 @@ class Ops:
 
     def key_le(self, x: int, y: int) -> bool:
         raise NotImplementedError
+
+    def upper_bound(self, a: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
+        """int64 tensor: number of keys of sorted `a` <= each value (key order)"""
+        raise NotImplementedError
+
+    def order(self, t: torch.Tensor) -> torch.Tensor:
+        """int64 view of int32-stored keys that is monotone in key order"""
+        f = 0x80000000 if getattr(self, "key", "u32") == "i32" else 0
+        return (t.to(torch.int64) & 0xFFFFFFFF) ^ f
 
 
 class HipOps(Ops):
@@ -74,6 +95,12 @@ class HipOps(Ops):
         f = 0x80000000 if self.key == "i32" else 0
         return ((x & 0xFFFFFFFF) ^ f) <= ((y & 0xFFFFFFFF) ^ f)
 
+    def upper_bound(self, a, values):
+        out = torch.empty(values.numel(), dtype=torch.int32, device=a.device)
+        self.ls.upper_bound(a, a.numel(), values.contiguous(), values.numel(), out, key=self.key,
+                            stream=self.stream)
+        return out.to(torch.int64)
+
 
 class P2PComm:
     """Pairwise exchange over torch.distributed point-to-point ops (RCCL on the GPU
@@ -88,6 +115,27 @@ class P2PComm:
         for r in dist.batch_isend_irecv(ops):
             r.wait()
 
+    def exchange_all(self, sends: list, recvs: list, rank: int) -> None:
+        """sends[j] -> rank j, recvs[j] <- rank j for every peer j != rank, all posted
+        together (one group: every xGMI link busy at once); empty pieces are skipped."""
+        g = self.group
+        ops = []
+        for j in range(len(sends)):
+            if j == rank:
+                continue
+            if sends[j].numel():
+                ops.append(dist.P2POp(dist.isend, sends[j], j, group=g))
+            if recvs[j].numel():
+                ops.append(dist.P2POp(dist.irecv, recvs[j], j, group=g))
+        if ops:
+            for r in dist.batch_isend_irecv(ops):
+                r.wait()
+
+    def all_gather(self, t: torch.Tensor) -> list:
+        out = [torch.empty_like(t) for _ in range(dist.get_world_size(self.group))]
+        dist.all_gather(out, t, group=self.group)
+        return out
+
 
 class HostStagedComm(P2PComm):
     """Test adapter: device tensors are staged through host memory and exchanged
@@ -99,6 +147,17 @@ class HostStagedComm(P2PComm):
         hr = torch.empty_like(hs)
         super().exchange(hs, hr, partner)
         recv.copy_(hr)
+
+    def exchange_all(self, sends, recvs, rank):
+        hs = [x.cpu() if j != rank else x[:0].cpu() for j, x in enumerate(sends)]
+        hr = [torch.empty(x.shape, dtype=x.dtype) if j != rank else x[:0].cpu() for j, x in enumerate(recvs)]
+        super().exchange_all(hs, hr, rank)
+        for j, (d, h) in enumerate(zip(recvs, hr)):
+            if j != rank and h.numel():
+                d.copy_(h)
+
+    def all_gather(self, t):
+        return [x.to(t.device) for x in super().all_gather(t.cpu())]
 
 
 def schedule(world: int):
@@ -190,3 +249,53 @@ def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, s
         else:
             a = ops.merge(got, a[k:], 0, m)       # partner's top k + my top m-k
     return a
+
+
+def dist_sort_splitters(local: torch.Tensor, ops: Ops, group=None, comm=None, copy_input: bool = False,
+                        oversample: int = 1024) -> torch.Tensor:
+    """Sort the global array whose rank-r shard is `local` with one all-peer exchange.
+    Returns this rank's contiguous range of the sorted array (ranges in rank order)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    comm = comm if comm is not None else P2PComm(group)
+    a = ops.local_sort(local, out_of_place=copy_input)
+    if world == 1:
+        return a
+    m = a.numel()
+    # regular sample of every sorted shard -> common splitters at the p-1 quantiles
+    s = oversample * world  # same sample size on every rank (all_gather), repeats if m < s
+    idx = (torch.arange(s, device=a.device, dtype=torch.int64) * m) // s
+    samp = a[idx].contiguous() if m else torch.zeros(s, dtype=a.dtype, device=a.device)
+    valid = torch.tensor([1 if m else 0], dtype=torch.int32, device=a.device)
+    samples = comm.all_gather(samp)
+    valids = torch.cat(comm.all_gather(valid)).cpu().tolist()  # ranks with an empty shard sample nothing
+    pool = torch.cat([x for x, v in zip(samples, valids) if v]) if any(valids) else samp
+    order = ops.order(pool)
+    srt = pool[torch.argsort(order, stable=True)]
+    q = (torch.arange(1, world, device=a.device, dtype=torch.int64) * srt.numel()) // world
+    splitters = srt[q].contiguous()
+    # cut points: piece j = keys in (splitter[j-1], splitter[j]]
+    cuts = ops.upper_bound(a, splitters) if m else torch.zeros(world - 1, dtype=torch.int64, device=a.device)
+    bounds = [0] + [int(c) for c in cuts.cpu().tolist()] + [m]
+    sizes = torch.tensor([bounds[j + 1] - bounds[j] for j in range(world)], dtype=torch.int64, device=a.device)
+    all_sizes = torch.stack(comm.all_gather(sizes)).cpu()  # all_sizes[i][j] = rank i -> rank j
+    sends = [a[bounds[j]:bounds[j + 1]] for j in range(world)]
+    recvs = [torch.empty(int(all_sizes[i][rank]), dtype=a.dtype, device=a.device) if i != rank else sends[rank]
+             for i in range(world)]
+    comm.exchange_all([x.contiguous() for x in sends], recvs, rank)
+    # merge the p sorted runs in rank order (merge tree, A before B on ties)
+    runs = [r for r in recvs]
+    while len(runs) > 1:
+        nxt = []
+        for i in range(0, len(runs) - 1, 2):
+            x, y = runs[i], runs[i + 1]
+            if x.numel() == 0:
+                nxt.append(y)
+            elif y.numel() == 0:
+                nxt.append(x)
+            else:
+                nxt.append(ops.merge(x, y, 0, x.numel() + y.numel()))
+        if len(runs) % 2:
+            nxt.append(runs[-1])
+        runs = nxt
+    return runs[0].contiguous()

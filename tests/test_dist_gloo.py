@@ -38,7 +38,13 @@ def _worker(rank, world, port, cfg, q):
 
         class NumpyOps(D.Ops):
             def __init__(self, key):
+                self.key = key
                 self.f = np.uint32(0x80000000 if key == "i32" else 0)
+
+            def upper_bound(self, a, values):
+                av = self._u(a)
+                vv = self._u(values)
+                return torch.from_numpy(np.searchsorted(av, vv, side="right").astype(np.int64))
 
             def _u(self, t):
                 return t.numpy().view(np.uint32) ^ self.f
@@ -62,8 +68,12 @@ def _worker(rank, world, port, cfg, q):
         m, dist_name, seed, key = cfg["m"], cfg["dist"], cfg["seed"], cfg["key"]
         shard = O.gen(m, seed, dist_name, first=rank * m)
         t = torch.from_numpy(shard.view(np.int32).copy())
-        out = D.dist_sort(t, NumpyOps(key), partial=cfg["partial"], stride=cfg["stride"],
-                          copy_input=cfg.get("copy", False))
+        if cfg.get("exchange") == "splitters":
+            out = D.dist_sort_splitters(t, NumpyOps(key), copy_input=cfg.get("copy", False),
+                                        oversample=cfg.get("oversample", 64))
+        else:
+            out = D.dist_sort(t, NumpyOps(key), partial=cfg["partial"], stride=cfg["stride"],
+                              copy_input=cfg.get("copy", False))
         if cfg.get("copy", False):
             assert torch.equal(t, torch.from_numpy(shard.view(np.int32)))  # input untouched
         q.put((rank, out.numpy().copy()))
@@ -92,6 +102,11 @@ CFGS = [
     dict(m=3000, dist="mod1000", seed=0x5EED0007, key="u32", partial=False, stride=64),
     dict(m=2000, dist="const", seed=1, key="u32", partial=True, stride=7),
     dict(m=2000, dist="reversed", seed=1, key="u32", partial=True, stride=128),
+    dict(m=5000, dist="u32", seed=0x5EED0008, key="u32", exchange="splitters", copy=True),
+    dict(m=4000, dist="mod100", seed=0x5EED0009, key="u32", exchange="splitters"),
+    dict(m=3001, dist="u32", seed=0x5EED000A, key="i32", exchange="splitters", oversample=3),
+    dict(m=100, dist="const", seed=3, key="u32", exchange="splitters"),
+    dict(m=1, dist="u32", seed=4, key="u32", exchange="splitters"),
 ]
 
 

@@ -40,8 +40,11 @@ def _worker(rank, world, port, cfg, q):
         t = torch.empty(m, dtype=torch.int32, device="cuda")
         ls.fill(t, m, cfg["seed"], cfg["dist"], first=rank * m)
         ops = D.HipOps(ls, key=cfg["key"], local_algo=cfg["algo"])
-        out = D.dist_sort(t, ops, partial=cfg["partial"], stride=cfg["stride"], copy_input=True,
-                          comm=D.HostStagedComm())
+        if cfg.get("exchange") == "splitters":
+            out = D.dist_sort_splitters(t, ops, copy_input=True, comm=D.HostStagedComm())
+        else:
+            out = D.dist_sort(t, ops, partial=cfg["partial"], stride=cfg["stride"], copy_input=True,
+                              comm=D.HostStagedComm())
         torch.cuda.synchronize()
         q.put((rank, out.cpu().numpy().copy()))
     finally:
@@ -67,6 +70,9 @@ CFGS = [
     dict(m=1 << 20, dist="u32", seed=0x5EED0005, key="u32", algo="radix", partial=True, stride=4096),
     dict(m=65_537, dist="mod100", seed=0x5EED0006, key="u32", algo="merge", partial=True, stride=1000),
     dict(m=50_000, dist="u32", seed=0x5EED0007, key="i32", algo="radix", partial=False, stride=64),
+    dict(m=1 << 20, dist="u32", seed=0x5EED0008, key="u32", algo="radix", exchange="splitters"),
+    dict(m=300_001, dist="mod1000", seed=0x5EED0009, key="i32", algo="radix", exchange="splitters"),
+    dict(m=70_000, dist="const", seed=0x5EED000A, key="u32", algo="radix", exchange="splitters"),
 ]
 
 
