@@ -20,6 +20,7 @@ constexpr int OSP_BLOCK = 512;
 constexpr int OSP_KPT = 16;
 constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 8192 keys per tile
 constexpr int OSP_LBW = 4;                     // look-back window (predecessor tiles per round)
+constexpr int OSP_DEFAULT_VARIANT = 2;          // see k_onesweep_p<LDS_MATCH, HIST_FIRST>
 constexpr int OSP_BLOCKS_PER_CU = 2;           // persistent grid = 2 x CUs (LDS ~59 KB, 127 VGPRs)
 static_assert(OSP_TILE == OS_TILE, "look-back layout shared with the 1-bit pass");
 

@@ -23,6 +23,8 @@
 //                     on equal keys) and an LDS merge per tile.
 #include "common.h"
 
+#include <cstdlib>
+
 namespace labsort {
 
 // ---------------------------------------------------------------------------------
@@ -50,6 +52,19 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d) {
         m &= bit ? bal : ~bal;
     }
     return m;
+}
+
+// Lanes whose 8-bit digit equals mine, XOR form (v_xor / v_or3 per ballot).
+__device__ __forceinline__ uint64_t match8(uint32_t d) {
+    uint32_t xlo = 0, xhi = 0;
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+        const int32_t sgn = ((int32_t)(d << (31 - b))) >> 31;  // 0 or -1: bit b of d
+        const uint64_t bal = __ballot(sgn != 0);
+        xlo |= (uint32_t)bal ^ (uint32_t)sgn;
+        xhi |= (uint32_t)(bal >> 32) ^ (uint32_t)sgn;
+    }
+    return ((uint64_t)~xhi << 32) | (uint64_t)~xlo;
 }
 
 // Exclusive scan over the first R threads of the block (value v in thread tid < R,
@@ -607,6 +622,10 @@ struct OspSmem {
 
 constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 
+// LDS_MATCH: peers of a digit by an LDS atomic-OR (else 8 ballots, VALU only);
+// HIST_FIRST: tile histogram by LDS atomics before ranking, aggregate published
+// early (else summed from the per-wave rank counters after ranking).
+template <bool LDS_MATCH, bool HIST_FIRST>
 __global__ __launch_bounds__(OSP_BLOCK, 2 * OSP_BLOCK / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
                                                           uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
                                                           uint32_t *lookback, uint32_t *counter, uint32_t *err,
@@ -681,20 +700,23 @@ __global__ __launch_bounds__(OSP_BLOCK, 2 * OSP_BLOCK / 256) void k_onesweep_p(B
             if (nvalidB == (uint32_t)TILE) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) kB[j] = src[j * WAVE];
+                if constexpr (HIST_FIRST) {
 #pragma unroll
-                for (int j = 0; j < KPT; ++j) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
+                    for (int j = 0; j < KPT; ++j) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
+                }
             } else {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const bool ok = woff + j * WAVE < nvalidB;
                     kB[j] = ok ? src[j * WAVE] : sentinel;
-                    if (ok) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
+                    if constexpr (HIST_FIRST)
+                        if (ok) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
                 }
             }
         }
-        __syncthreads();  // (1) histogram of B complete
+        if constexpr (HIST_FIRST) __syncthreads();  // (1) histogram of B complete
         if (haveB) {
-            if (tid < (uint32_t)R) {
+            if (HIST_FIRST && tid < (uint32_t)R) {
                 hB = sm.hist[tid];
                 st_agent(lookback + (size_t)slotB * R + tid, (lB == 0 ? LB_INC : LB_AGG) | hB);
                 xB = hB;
@@ -709,10 +731,15 @@ __global__ __launch_bounds__(OSP_BLOCK, 2 * OSP_BLOCK / 256) void k_onesweep_p(B
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
-                uint64_t *slot = wm + d;
-                __hip_atomic_fetch_or(slot, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                const uint64_t m = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                uint64_t m;
+                if constexpr (LDS_MATCH) {
+                    uint64_t *slot = wm + d;
+                    __hip_atomic_fetch_or(slot, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    m = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                } else {
+                    m = match8(d);
+                }
                 const uint32_t pre = mbcnt64(m);
                 const uint32_t old = wh[d];
                 if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
@@ -754,6 +781,24 @@ __global__ __launch_bounds__(OSP_BLOCK, 2 * OSP_BLOCK / 256) void k_onesweep_p(B
             sm.delta[tid] = sp->base[segA * R + tid] + excl - dstartA;
         }
         __syncthreads();  // (2) delta of A, wave counts and wsum of B
+        if (!HIST_FIRST && haveB) {
+            // tile histogram = sum of the per-wave counts; publish B's aggregate, scan it
+            if (tid < (uint32_t)R) {
+                uint32_t tot = 0;
+#pragma unroll
+                for (int w = 0; w < W; ++w) tot += sm.wh[w * R + tid];
+                if (tid == (uint32_t)R - 1) tot -= (uint32_t)TILE - nvalidB;  // sentinels
+                hB = tot;
+                st_agent(lookback + (size_t)slotB * R + tid, (lB == 0 ? LB_INC : LB_AGG) | hB);
+                xB = hB;
+#pragma unroll
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t t = __shfl_up(xB, off);
+                    if (lane >= (uint32_t)off) xB += t;
+                }
+                if (lane == 63) sm.wsum[wid] = xB;
+            }
+        }
         if (slotA != OSP_DONE) {
             if (nvalidA == (uint32_t)TILE) {
 #pragma unroll
@@ -770,6 +815,7 @@ __global__ __launch_bounds__(OSP_BLOCK, 2 * OSP_BLOCK / 256) void k_onesweep_p(B
             }
         }
         if (!haveB) break;
+        if constexpr (!HIST_FIRST) __syncthreads();  // (2b) wsum of B
         if (tid < (uint32_t)R) {
             uint32_t add = 0;
 #pragma unroll
@@ -793,7 +839,8 @@ __global__ __launch_bounds__(OSP_BLOCK, 2 * OSP_BLOCK / 256) void k_onesweep_p(B
         __syncthreads();  // (4) B reordered in LDS
 #pragma unroll
         for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[j * OSP_BLOCK + tid];
-        for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) sm.wh[i] = 0u;
+        // each wave clears its own counters (no barrier before the next ranking)
+        for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
         if (count_next) {  // (top nibble of this digit, next active digit) of B's valid keys
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
@@ -1155,7 +1202,17 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
     const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE + NSEG;
     const size_t want = (size_t)OSP_BLOCKS_PER_CU * cu_count();
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
-    k_onesweep_p<<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint);
+    static int variant = -1;
+    if (variant < 0) {  // LABSORT_OSP=<lds match 0/1><hist first 0/1>; default "10" (measured fastest, r06)
+        const char *e = std::getenv("LABSORT_OSP");
+        variant = (e && e[0] && e[1]) ? ((e[0] == '1') << 1) | (e[1] == '1') : OSP_DEFAULT_VARIANT;
+    }
+    switch (variant) {
+    case 3: k_onesweep_p<true, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 2: k_onesweep_p<true, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 1: k_onesweep_p<false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    default: k_onesweep_p<false, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    }
     return hipGetLastError();
 }
 
