@@ -46,7 +46,7 @@ constexpr int TS_TILE = TS_BLOCK * TS_KPT;  // 8192-key sorted runs
 
 // ---- merge path ----
 constexpr int MG_BLOCK = 256;
-constexpr int MG_KPT = 16;
+constexpr int MG_KPT = 8;
 constexpr int MG_TILE = MG_BLOCK * MG_KPT;  // 4096 outputs per workgroup
 
 constexpr int MAX_PASSES = 32;
