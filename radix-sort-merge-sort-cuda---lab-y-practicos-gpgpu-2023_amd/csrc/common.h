@@ -47,7 +47,8 @@ constexpr int TS_TILE = TS_BLOCK * TS_KPT;  // 8192-key sorted runs
 // ---- merge path ----
 constexpr int MG_BLOCK = 256;
 constexpr int MG_KPT = 8;
-constexpr int MG_TILE = MG_BLOCK * MG_KPT;  // 4096 outputs per workgroup
+constexpr int MG_TILE = MG_BLOCK * MG_KPT;
+constexpr int MG_BLOCKS_PER_CU = 8;  // persistent merge pass grid  // 4096 outputs per workgroup
 
 constexpr int MAX_PASSES = 32;
 constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_SKIP = 0xFFu;

@@ -1077,6 +1077,101 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass(const uint32_t *__restrict
     merge_tile<BLOCK, KPT>(src + g.pb, a0, a1, src + g.pb + g.la, b0, b1, dst + o0, flip, sm);
 }
 
+// Persistent, software-pipelined merge pass: workgroup b merges output tiles
+// b, b+G, b+2G, ...; the keys of the next tile are loaded into registers while the
+// current tile is merged in LDS, and the co-ranks two tiles ahead, so the global
+// load latency hides behind the LDS merge instead of stalling every tile.
+template <int BLOCK, int KPT>
+__global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                                        uint32_t n, uint32_t run, uint32_t flip,
+                                                        const uint32_t *__restrict__ part, uint32_t ntiles) {
+    constexpr uint32_t T = (uint32_t)(BLOCK * KPT);
+    static_assert(T == (uint32_t)MG_TILE, "partition granularity");
+    __shared__ MgSmem sm;
+    const uint32_t tid = threadIdx.x, G = gridDim.x;
+    struct Geo {
+        uint32_t o0, tot, la, sa, sb;  // output start, keys, A keys, A start, B start (absolute)
+    };
+    auto geo = [&](uint32_t t, uint32_t p0, uint32_t p1) {
+        Geo q;
+        q.o0 = t * T;
+        const uint32_t o1 = (n - q.o0) < T ? n : q.o0 + T;
+        const PairGeom g = pair_of(q.o0, n, run);
+        const uint32_t a0 = p0;
+        const uint32_t a1 = (o1 - g.pb == g.la + g.lb) ? g.la : p1;
+        const uint32_t b0 = (q.o0 - g.pb) - a0, b1 = (o1 - g.pb) - a1;
+        q.tot = o1 - q.o0;
+        q.la = a1 - a0;
+        q.sa = g.pb + a0;
+        q.sb = g.pb + g.la + b0;
+        (void)b1;
+        return q;
+    };
+    auto load = [&](const Geo &q, uint32_t (&v)[KPT]) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t k = tid + (uint32_t)j * BLOCK;
+            v[j] = k < q.tot ? src[k < q.la ? q.sa + k : q.sb + (k - q.la)] : 0u;
+        }
+    };
+    uint32_t t = blockIdx.x;
+    if (t >= ntiles) return;
+    uint32_t nx[KPT];
+    Geo cur = geo(t, part[t], part[t + 1]);
+    load(cur, nx);
+    uint32_t t2 = t + G;  // co-ranks of the tile after this one
+    uint32_t q0 = t2 < ntiles ? part[t2] : 0u, q1 = t2 < ntiles ? part[t2 + 1] : 0u;
+    for (; t < ntiles; t += G) {
+        __syncthreads();  // previous tile's merge no longer reads sm.in
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
+        // next tile: geometry from the prefetched co-ranks, keys into registers
+        const uint32_t tn = t + G;
+        Geo nxt = cur;
+        if (tn < ntiles) {
+            nxt = geo(tn, q0, q1);
+            load(nxt, nx);
+            const uint32_t t3 = tn + G;
+            q0 = t3 < ntiles ? part[t3] : 0u;
+            q1 = t3 < ntiles ? part[t3 + 1] : 0u;
+        }
+        __syncthreads();  // sm.in holds the current tile
+        const uint32_t la = cur.la, lb = cur.tot - cur.la, tot = cur.tot;
+        const uint32_t *sa = sm.in, *sb = sm.in + la;
+        const uint32_t d = tid * KPT < tot ? tid * KPT : tot;
+        uint32_t ai = corank(sa, la, sb, lb, d, flip);
+        uint32_t bi = d - ai;
+        uint32_t va = ai < la ? sa[ai] : 0u;
+        uint32_t vb = bi < lb ? sb[bi] : 0u;
+        uint32_t r[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const bool takeA = (bi >= lb) || (ai < la && key_le(va, vb, flip));
+            r[j] = takeA ? va : vb;
+            if (takeA) {
+                ++ai;
+                va = ai < la ? sa[ai] : 0u;
+            } else {
+                ++bi;
+                vb = bi < lb ? sb[bi] : 0u;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = tid * KPT + j;
+            if (idx < tot) sm.out[idx + (idx >> 5)] = r[j];
+        }
+        __syncthreads();
+        uint32_t *__restrict__ o = dst + cur.o0;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t i = tid + (uint32_t)j * BLOCK;
+            if (i < tot) o[i] = sm.out[i + (i >> 5)];
+        }
+        cur = nxt;
+    }
+}
+
 // two separate arrays, diagonal range [d0, d1): part has ntiles+1 entries
 __global__ __launch_bounds__(256) void k_merge_part_ab(const uint32_t *__restrict__ A, uint32_t la,
                                                        const uint32_t *__restrict__ B, uint32_t lb, uint32_t d0,
@@ -1260,7 +1355,10 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
     k_merge_part_pass<<<(ntiles + 255) / 256, 256, 0, s>>>(in, (uint32_t)n, (uint32_t)run, flip, part, ntiles);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    k_merge_pass<MG_BLOCK, MG_KPT><<<ntiles, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, part);
+    const unsigned want = (unsigned)(MG_BLOCKS_PER_CU * cu_count());
+    k_merge_pass_p<MG_BLOCK, MG_KPT><<<ntiles < want ? ntiles : want, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n,
+                                                                                        (uint32_t)run, flip, part,
+                                                                                        ntiles);
     return hipGetLastError();
 }
 
