@@ -872,6 +872,7 @@ struct TsSmem {
     static constexpr int R = 256, W = BLOCK / WAVE, TILE = BLOCK * KPT;
     uint32_t keys[TILE];
     uint32_t whist[W * R];
+    uint64_t match[W * R];
     uint32_t dstart[R];
     uint32_t wsum[W];
     uint32_t red_and[W];
@@ -921,14 +922,27 @@ __global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_
         diff = aa ^ oo;
     }
     uint32_t *wh = sm.whist + wid * R;
+    uint64_t *wm = sm.match + wid * R;
+    for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wm[i] = 0ull;
     for (int pass = 0; pass < 4; ++pass) {
         const uint32_t shift = pass * 8;
         if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the block
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
         uint32_t dig[KPT], rank[KPT];
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) dig[j] = ((k[j] ^ flip) >> shift) & 0xFFu;
-        wave_rank<8, KPT>(dig, rank, wh);
+        for (int j = 0; j < KPT; ++j) {
+            // stable wave rank; peers of a digit by an LDS atomic-OR of lane bits
+            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+            uint64_t *slot = wm + d;
+            __hip_atomic_fetch_or(slot, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const uint64_t m = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const uint32_t pre = mbcnt64(m);
+            const uint32_t old = wh[d];
+            if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
+            dig[j] = d;
+            rank[j] = old + pre;
+        }
         __syncthreads();
         uint32_t tot = 0;
         if (tid < (uint32_t)R) {
