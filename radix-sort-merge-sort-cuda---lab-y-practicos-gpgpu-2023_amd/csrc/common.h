@@ -16,13 +16,13 @@ constexpr int OS_TILE = OS_BLOCK * OS_KPT;  // 8192 keys per tile
 constexpr int HIST_BLOCK = 1024;
 
 // ---- persistent pipelined onesweep (8-bit digits) ----
-constexpr int OSP_BLOCK = 512;
+constexpr int OSP_BLOCK = 1024;
 constexpr int OSP_KPT = 16;
-constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 8192 keys per tile
+constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 16384 keys per tile
 constexpr int OSP_LBW = 4;                     // look-back window (predecessor tiles per round)
 constexpr int OSP_DEFAULT_VARIANT = 2;          // see k_onesweep_p<LDS_MATCH, HIST_FIRST>
-constexpr int OSP_BLOCKS_PER_CU = 2;           // persistent grid = 2 x CUs (LDS ~59 KB, 127 VGPRs)
-static_assert(OSP_TILE == OS_TILE, "look-back layout shared with the 1-bit pass");
+constexpr int OSP_BLOCKS_PER_CU = 1;           // persistent grid = CUs (16-wave workgroups, LDS ~130 KB, 128 VGPRs)
+static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass tiles");
 
 // ---- segmented look-back chains (8-bit radix) ----
 // Each pass's input is split into NSEG contiguous segments, each with its own

@@ -626,13 +626,13 @@ constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 // HIST_FIRST: tile histogram by LDS atomics before ranking, aggregate published
 // early (else summed from the per-wave rank counters after ranking).
 template <bool LDS_MATCH, bool HIST_FIRST>
-__global__ __launch_bounds__(OSP_BLOCK, 2 * OSP_BLOCK / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
+__global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
                                                           uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
                                                           uint32_t *lookback, uint32_t *counter, uint32_t *err,
                                                           uint32_t *__restrict__ joint) {
     using S = OspSmem;
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW;
-    static_assert(OSP_BLOCK == 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
+    static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
     __shared__ S sm;
 
     const uint32_t srcsel = plan->src[pass];
