@@ -153,8 +153,10 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
     uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
     uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
     Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
-    HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.zero_bytes, s));
     if (bits == 8) {
+        // histograms first; the look-back words (tens of MB) are cleared after the
+        // histogram so their dirty lines do not compete with its read of the keys
+        HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.off_lookback - L.off_hist, s));
         uint32_t *hps = reinterpret_cast<uint32_t *>(ws + L.off_hps);
         uint32_t *joint = reinterpret_cast<uint32_t *>(ws + L.off_joint);
         SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
@@ -162,6 +164,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
             HIP_TRY(launch_hist_seg(in, n, flip, hps, s));
         }
+        HIP_TRY(hipMemsetAsync(ws + L.off_lookback, 0, L.off_hist + L.zero_bytes - L.off_lookback, s));
         HIP_TRY(launch_plan8(hps, n, in == out ? 1 : 0, plan, sps, hist, s));
         for (int p = 0; p < L.P; ++p) {
             if (p > 0) HIP_TRY(launch_segplan(plan, p, n, hist, joint, sps, s));
@@ -170,6 +173,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
                                       counters + p, err, joint, s));
         }
     } else {
+        HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.zero_bytes, s));
         {
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
             HIP_TRY(launch_histogram(in, n, flip, bits, hist, s));
