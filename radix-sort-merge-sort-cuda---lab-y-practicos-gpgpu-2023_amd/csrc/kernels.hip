@@ -67,6 +67,16 @@ __device__ __forceinline__ uint64_t match8(uint32_t d) {
     return ((uint64_t)~xhi << 32) | (uint64_t)~xlo;
 }
 
+// Lanes of this wave whose digit selects the same LDS slot as mine, by an atomic XOR
+// of lane bits: the slot changes by exactly the peers' bits whatever it held, so it
+// needs no clearing (a read before and after instead of an OR, a read and a 64-bit
+// clearing store).  LDS operations of one wave complete in issue order.
+__device__ __forceinline__ uint64_t lds_peers(uint64_t *slot, uint32_t lane) {
+    const uint64_t before = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_fetch_xor(slot, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return before ^ __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 // Exclusive scan over the first R threads of the block (value v in thread tid < R,
 // others pass 0).  Must be called by every thread (contains a barrier when R > 64).
 template <int BLOCK, int R>
@@ -600,7 +610,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
 //   * the tile's digit histogram is built first (LDS atomics) and its aggregate
 //     published before ranking, so successors see it early;
 //   * the look-back reads a window of OSP_LBW predecessors per round;
-//   * the stable wave rank uses an LDS atomic-OR match (one 64-bit lane mask per
+//   * the stable wave rank uses an LDS atomic-XOR match (one 64-bit lane mask per
 //     digit and wave) instead of 8 ballots per key slot.
 // Dynamic tile ids (atomic counter) order the tiles by acquisition, so a tile only
 // ever waits on tiles whose aggregates are published unconditionally right after
@@ -622,7 +632,7 @@ struct OspSmem {
 
 constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 
-// LDS_MATCH: peers of a digit by an LDS atomic-OR (else 8 ballots, VALU only);
+// LDS_MATCH: peers of a digit by an LDS atomic-XOR (else 8 ballots, VALU only);
 // HIST_FIRST: tile histogram by LDS atomics before ranking, aggregate published
 // early (else summed from the per-wave rank counters after ranking).
 template <bool LDS_MATCH, bool HIST_FIRST>
@@ -647,10 +657,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     const bool count_next = nxt != NEXT_NONE;
     const uint32_t nshift = count_next ? nxt * 8u : 0u;
 
-    for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) {
-        sm.wh[i] = 0u;
-        sm.match[i] = 0ull;
-    }
+    for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) sm.wh[i] = 0u;
     for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += OSP_BLOCK) sm.joint[i] = 0u;
     if (tid <= (uint32_t)NSEG) {
         sm.start[tid] = sp->start[tid];
@@ -727,16 +734,13 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                 }
                 if (lane == 63) sm.wsum[wid] = xB;
             }
-            // stable wave rank of B: lanes sharing a digit found by an LDS atomic-OR
+            // stable wave rank of B: lanes sharing a digit found by an LDS atomic-XOR
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
                 uint64_t m;
                 if constexpr (LDS_MATCH) {
-                    uint64_t *slot = wm + d;
-                    __hip_atomic_fetch_or(slot, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    m = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-                    __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    m = lds_peers(wm + d, lane);
                 } else {
                     m = match8(d);
                 }
@@ -923,7 +927,6 @@ __global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_
     }
     uint32_t *wh = sm.whist + wid * R;
     uint64_t *wm = sm.match + wid * R;
-    for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wm[i] = 0ull;
     for (int pass = 0; pass < 4; ++pass) {
         const uint32_t shift = pass * 8;
         if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the block
@@ -931,12 +934,9 @@ __global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_
         uint32_t dig[KPT], rank[KPT];
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            // stable wave rank; peers of a digit by an LDS atomic-OR of lane bits
+            // stable wave rank; peers of a digit by an LDS atomic-XOR of lane bits
             const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-            uint64_t *slot = wm + d;
-            __hip_atomic_fetch_or(slot, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            const uint64_t m = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            const uint64_t m = lds_peers(wm + d, lane);
             const uint32_t pre = mbcnt64(m);
             const uint32_t old = wh[d];
             if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
