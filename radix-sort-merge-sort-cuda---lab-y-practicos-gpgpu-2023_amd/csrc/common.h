@@ -20,7 +20,8 @@ constexpr int OSP_BLOCK = 1024;
 constexpr int OSP_KPT = 16;
 constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 16384 keys per tile
 constexpr int OSP_LBW = 4;                     // look-back window (predecessor tiles per round)
-constexpr int OSP_DEFAULT_VARIANT = 2;          // see k_onesweep_p<LDS_MATCH, HIST_FIRST>
+constexpr int OSP_RANK_BALLOT = 0, OSP_RANK_MATCH = 1, OSP_RANK_ATOMIC = 2;  // k_onesweep_p<RANK, HIST_FIRST>
+constexpr int OSP_DEFAULT_VARIANT = 4;          // variant = RANK * 2 + HIST_FIRST
 constexpr int OSP_BLOCKS_PER_CU = 1;           // persistent grid = CUs (16-wave workgroups, LDS ~130 KB, 128 VGPRs)
 static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass tiles");
 

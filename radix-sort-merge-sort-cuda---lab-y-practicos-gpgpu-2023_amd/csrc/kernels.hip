@@ -77,6 +77,26 @@ __device__ __forceinline__ uint64_t lds_peers(uint64_t *slot, uint32_t lane) {
     return before ^ __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// True (in every lane) if one returning LDS atomic add instruction services the lanes
+// that hit one address in ascending lane order, on five sharing patterns (all lanes,
+// contiguous groups, strided groups, two scrambled ones).  Call with the whole wave
+// active; `scratch` = 64 words of LDS private to the wave.
+__device__ __forceinline__ bool lds_lane_ordered(uint32_t *scratch, uint32_t lane) {
+    bool ok = true;
+#pragma unroll
+    for (int p = 0; p < 5; ++p) {
+        const uint32_t a = p == 0 ? 0u
+                         : p == 1 ? lane >> 3
+                         : p == 2 ? lane & 7u
+                         : p == 3 ? ((lane * 37u) ^ (lane >> 2)) & 15u
+                                  : ((lane * 0x9E37u) >> 5) & 3u;
+        __hip_atomic_store(scratch + lane, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        const uint32_t got = __hip_atomic_fetch_add(scratch + a, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        ok &= got == mbcnt64(match_digit<6>(a));
+    }
+    return __ballot(!ok) == 0ull;
+}
+
 // Exclusive scan over the first R threads of the block (value v in thread tid < R,
 // others pass 0).  Must be called by every thread (contains a barrier when R > 64).
 template <int BLOCK, int R>
@@ -616,11 +636,14 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
 // ever waits on tiles whose aggregates are published unconditionally right after
 // their histogram: forward progress holds for any grid size or residency.
 // ---------------------------------------------------------------------------------
+template <bool MATCH>
 struct OspSmem {
     static constexpr int R = 256, W = OSP_BLOCK / WAVE, TILE = OSP_TILE;
     uint32_t keys[TILE];
     uint32_t wh[W * R];
-    uint64_t match[W * R];
+    uint64_t match[MATCH ? W * R : 1];
+    uint32_t probe[WAVE];
+    uint32_t ordered;
     uint32_t hist[R];
     uint32_t delta[R];
     uint32_t start[NSEG + 1];
@@ -632,15 +655,23 @@ struct OspSmem {
 
 constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 
-// LDS_MATCH: peers of a digit by an LDS atomic-XOR (else 8 ballots, VALU only);
+// RANK: how a wave ranks its keys stably per digit:
+//   OSP_RANK_BALLOT: peers of a digit by 8 ballots (VALU only), counter read + update;
+//   OSP_RANK_MATCH:  peers by an LDS atomic-XOR of lane bits, counter read + update;
+//   OSP_RANK_ATOMIC: one returning LDS atomic add per key on the wave's counter.  The
+//                    rank is stable because gfx950's LDS services the lanes of one
+//                    atomic instruction that hit one address in ascending lane order.
+//                    The ISA does not promise that order, so every workgroup first
+//                    checks it (lds_lane_ordered) and ranks by OSP_RANK_MATCH if the
+//                    check fails.
 // HIST_FIRST: tile histogram by LDS atomics before ranking, aggregate published
 // early (else summed from the per-wave rank counters after ranking).
-template <bool LDS_MATCH, bool HIST_FIRST>
+template <int RANK, bool HIST_FIRST>
 __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
                                                           uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
                                                           uint32_t *lookback, uint32_t *counter, uint32_t *err,
                                                           uint32_t *__restrict__ joint) {
-    using S = OspSmem;
+    using S = OspSmem<RANK != OSP_RANK_BALLOT>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW;
     static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
     __shared__ S sm;
@@ -675,8 +706,13 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         }
     };
     if (tid == 0) sm.next = acquire();
+    if (RANK == OSP_RANK_ATOMIC && wid == 0) {
+        const bool ord = lds_lane_ordered(sm.probe, lane);
+        if (lane == 0) sm.ordered = ord ? 1u : 0u;
+    }
     __syncthreads();
     uint32_t cB = sm.next;
+    const bool atomic_rank = RANK == OSP_RANK_ATOMIC && __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
 
     // carried state of tile A (slot = look-back slot, lo = slot of its segment's first tile)
     uint32_t slotA = OSP_DONE, loA = 0, segA = 0, nvalidA = 0;
@@ -738,16 +774,15 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
-                uint64_t m;
-                if constexpr (LDS_MATCH) {
-                    m = lds_peers(wm + d, lane);
+                if (atomic_rank) {
+                    rB[j] = (__hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) << 8) | d;
                 } else {
-                    m = match8(d);
+                    const uint64_t m = RANK != OSP_RANK_BALLOT ? lds_peers(wm + d, lane) : match8(d);
+                    const uint32_t pre = mbcnt64(m);
+                    const uint32_t old = wh[d];
+                    if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
+                    rB[j] = ((old + pre) << 8) | d;
                 }
-                const uint32_t pre = mbcnt64(m);
-                const uint32_t old = wh[d];
-                if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
-                rB[j] = ((old + pre) << 8) | d;
             }
         }
         // complete the look-back of A; publish its inclusive prefix (within its segment)
@@ -1312,15 +1347,18 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
     const size_t want = (size_t)OSP_BLOCKS_PER_CU * cu_count();
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
     static int variant = -1;
-    if (variant < 0) {  // LABSORT_OSP=<lds match 0/1><hist first 0/1>; default "10" (measured fastest, r06)
+    if (variant < 0) {  // LABSORT_OSP=<rank 0/1/2><hist first 0/1>; default OSP_DEFAULT_VARIANT
         const char *e = std::getenv("LABSORT_OSP");
-        variant = (e && e[0] && e[1]) ? ((e[0] == '1') << 1) | (e[1] == '1') : OSP_DEFAULT_VARIANT;
+        variant = (e && e[0] >= '0' && e[0] <= '2' && e[1]) ? ((e[0] - '0') << 1) | (e[1] == '1') : OSP_DEFAULT_VARIANT;
     }
     switch (variant) {
-    case 3: k_onesweep_p<true, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
-    case 2: k_onesweep_p<true, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
-    case 1: k_onesweep_p<false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
-    default: k_onesweep_p<false, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 0: k_onesweep_p<0, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 1: k_onesweep_p<0, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 2: k_onesweep_p<1, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 3: k_onesweep_p<1, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 4: k_onesweep_p<2, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 5: k_onesweep_p<2, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }

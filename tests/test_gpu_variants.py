@@ -1,4 +1,4 @@
-"""Every compiled variant of the onesweep pass (LABSORT_OSP=<lds match><hist first>,
+"""Every compiled variant of the onesweep pass (LABSORT_OSP=<rank: ballot 0, LDS match 1, LDS atomic 2><hist first>,
 read once per process) sorts correctly: each variant runs in its own subprocess on
 cuda:0 over sizes/distributions that exercise partial tiles, trivial passes and
 the digit-group segments, checked against std::sort (the oracle)."""
@@ -32,7 +32,7 @@ print("ok")
 '''
 
 
-@pytest.mark.parametrize("variant", ["00", "01", "10", "11"])
+@pytest.mark.parametrize("variant", ["00", "01", "10", "11", "20", "21"])
 def test_onesweep_variant(oracle, variant):
     env = dict(os.environ, LABSORT_OSP=variant)
     r = subprocess.run([sys.executable, "-c", SCRIPT, REPO], env=env, capture_output=True, text=True, timeout=300)
