@@ -21,6 +21,7 @@ constexpr int OSP_KPT = 16;
 constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 16384 keys per tile
 constexpr int OSP_LBW = 4;                     // look-back window (predecessor tiles per round)
 constexpr int OSP_RANK_BALLOT = 0, OSP_RANK_MATCH = 1, OSP_RANK_ATOMIC = 2;  // k_onesweep_p<RANK, HIST_FIRST>
+constexpr int OSP_SEG_LATER = 0;  // 1: digit-group segments after the first active pass (LABSORT_SEG)
 constexpr int OSP_DEFAULT_VARIANT = 4;          // variant = RANK * 2 + HIST_FIRST
 constexpr int OSP_BLOCKS_PER_CU = 1;           // persistent grid = CUs (16-wave workgroups, LDS ~130 KB, 128 VGPRs)
 static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass tiles");
@@ -36,7 +37,8 @@ struct SegPlan {
     uint32_t tpre[NSEG + 1];   // tiles in segments < s = look-back slot of segment s's first tile
     uint32_t maxt;             // most tiles in one segment
     uint32_t mode;             // 0 position segments, 1 digit-group segments, 2 one segment
-    uint32_t pad[12];
+    uint32_t segbits;          // tile id c -> segment c & (2^segbits - 1), tile c >> segbits
+    uint32_t pad[11];
     uint32_t base[NSEG * 256];  // output offset of the first key of digit d in segment s
 };
 

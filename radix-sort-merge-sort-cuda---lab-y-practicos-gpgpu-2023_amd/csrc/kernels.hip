@@ -24,6 +24,7 @@
 #include "common.h"
 
 #include <cstdlib>
+#include <cstring>
 
 namespace labsort {
 
@@ -377,13 +378,14 @@ __device__ void build_segplan(SegPlan *__restrict__ sp, const uint32_t *__restri
         }
         sp->maxt = mx;
         sp->mode = mode;
+        sp->segbits = mode == 2u ? 0u : 4u;
     }
 }
 
 // Pass plan for the 8-bit radix (as k_plan: totals, trivial passes, ping-pong
 // buffers; plus each pass's next active digit) and the first active pass's SegPlan.
 __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps, uint32_t n, int in_is_out,
-                                               Plan *__restrict__ plan, SegPlan *__restrict__ sps,
+                                               int seg_later, Plan *__restrict__ plan, SegPlan *__restrict__ sps,
                                                uint32_t *__restrict__ hist_out) {
     __shared__ uint32_t hist[4 * 256];
     __shared__ uint32_t sh[NSEG * 256 + 8];
@@ -403,7 +405,7 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
         hist_out[p * 256 + t] = v[p];
         if (v[p] == n) triv[p] = 1;
     }
-    if (t <= (uint32_t)NSEG) start[t] = (uint32_t)((size_t)t * n / NSEG);
+    if (t <= (uint32_t)NSEG) start[t] = seg_later < 0 ? (t ? n : 0u) : (uint32_t)((size_t)t * n / NSEG);
     __syncthreads();
     if (t == 0) {
         int act[4];
@@ -415,7 +417,8 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
         }
         for (int p = 0; p < 4; ++p)
             if (!triv[p]) act[k++] = p;
-        for (int i = 0; i + 1 < k; ++i) plan->next[act[i]] = (uint32_t)act[i + 1];
+        if (seg_later > 0)
+            for (int i = 0; i + 1 < k; ++i) plan->next[act[i]] = (uint32_t)act[i + 1];
         plan->active = (uint32_t)k;
         first = k ? act[0] : -1;
         if (k == 0) {
@@ -442,6 +445,12 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
     __syncthreads();
     if (first < 0) return;
     // first active pass: position segments; hs[s][d] = hps[s][first][d]
+    if (seg_later < 0) {  // one chain
+        for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[first * 256 + t];
+        __syncthreads();
+        build_segplan(sps + first, sh, start, 2u, sh);
+        return;
+    }
     for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = hps[s * 1024 + first * 256 + t];
     __syncthreads();
     build_segplan(sps + first, sh, start, 0u, sh);
@@ -450,7 +459,7 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
 // SegPlan of pass q when q is active and not the first: segments = ranges of the
 // previous active digit's top nibble (starts from its histogram), histograms from
 // the joint counts the previous pass wrote.
-__global__ __launch_bounds__(256) void k_segplan(const Plan *__restrict__ plan, int q, uint32_t n,
+__global__ __launch_bounds__(256) void k_segplan(const Plan *__restrict__ plan, int q, uint32_t n, int seg_later,
                                                  const uint32_t *__restrict__ hist, const uint32_t *__restrict__ joint,
                                                  SegPlan *__restrict__ sps) {
     __shared__ uint32_t sh[NSEG * 256 + 8];
@@ -458,6 +467,13 @@ __global__ __launch_bounds__(256) void k_segplan(const Plan *__restrict__ plan, 
     const uint32_t prev = plan->prev[q];
     if (plan->src[q] == SEL_SKIP || prev == NEXT_NONE) return;
     const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
+    if (seg_later <= 0) {  // one chain over the whole input
+        for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[q * 256 + t];
+        if (t <= (uint32_t)NSEG) start[t] = t ? n : 0u;
+        __syncthreads();
+        build_segplan(sps + q, sh, start, 2u, sh);
+        return;
+    }
     // segment starts: exclusive prefix over nibble groups of hist[prev]
     const uint32_t v = hist[prev * 256 + t];
     uint32_t x = v;
@@ -683,7 +699,8 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t shift = (uint32_t)pass * 8u;
     const uint32_t sentinel = ~flip;  // digit 255 in every pass: ranks after all real keys
-    const uint32_t climit = NSEG * sp->maxt;
+    const uint32_t segbits = sp->segbits, segmask = (1u << segbits) - 1u;
+    const uint32_t climit = sp->maxt << segbits;
     const uint32_t nxt = plan->next[pass];
     const bool count_next = nxt != NEXT_NONE;
     const uint32_t nshift = count_next ? nxt * 8u : 0u;
@@ -701,7 +718,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         for (;;) {
             const uint32_t c = atomicAdd(counter, 1u);
             if (c >= climit) return OSP_DONE;
-            const uint32_t sg = c & (NSEG - 1), l = c >> 4;
+            const uint32_t sg = c & segmask, l = c >> segbits;
             if (l < sp->tpre[sg + 1] - sp->tpre[sg]) return c;
         }
     };
@@ -723,7 +740,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     uint64_t *wm = sm.match + wid * R;
     for (;;) {
         const bool haveB = cB != OSP_DONE;
-        const uint32_t segB = cB & (NSEG - 1), lB = cB >> 4;
+        const uint32_t segB = cB & segmask, lB = cB >> segbits;
         const uint32_t loB = haveB ? sm.tpre[segB] : 0u, slotB = loB + lB;
         const uint32_t begB = haveB ? sm.start[segB] + lB * (uint32_t)TILE : 0u;
         const uint32_t endB = haveB ? sm.start[segB + 1] : 0u;
@@ -916,6 +933,8 @@ struct TsSmem {
     uint32_t wsum[W];
     uint32_t red_and[W];
     uint32_t red_or[W];
+    uint32_t probe[WAVE];
+    uint32_t ordered;
 };
 
 template <int BLOCK, int KPT>
@@ -949,7 +968,12 @@ __global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_
         sm.red_and[wid] = a;
         sm.red_or[wid] = o;
     }
+    if (wid == 0) {  // lane-ordered LDS atomics (see k_onesweep_p): rank by one atomic per key
+        const bool ord = lds_lane_ordered(sm.probe, lane);
+        if (lane == 0) sm.ordered = ord ? 1u : 0u;
+    }
     __syncthreads();
+    const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
     uint32_t diff = 0;
     {
         uint32_t aa = ~0u, oo = 0u;
@@ -969,14 +993,18 @@ __global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_
         uint32_t dig[KPT], rank[KPT];
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            // stable wave rank; peers of a digit by an LDS atomic-XOR of lane bits
+            // stable wave rank: lane-ordered returning atomic, else peers by an LDS atomic-XOR
             const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-            const uint64_t m = lds_peers(wm + d, lane);
-            const uint32_t pre = mbcnt64(m);
-            const uint32_t old = wh[d];
-            if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
             dig[j] = d;
-            rank[j] = old + pre;
+            if (atomic_rank) {
+                rank[j] = __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            } else {
+                const uint64_t m = lds_peers(wm + d, lane);
+                const uint32_t pre = mbcnt64(m);
+                const uint32_t old = wh[d];
+                if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
+                rank[j] = old + pre;
+            }
         }
         __syncthreads();
         uint32_t tot = 0;
@@ -1369,15 +1397,32 @@ hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32
     return hipGetLastError();
 }
 
+// Look-back chains per pass (LABSORT_SEG, read once per process):
+//   "first" (default): NSEG position segments in the first active pass, one chain in
+//            the later passes (no joint histograms counted);
+//   "on":    also digit-group segments in the later passes (joint histograms);
+//   "none":  one chain in every pass.
+// Measured on MI355X at 2^28 (r09): the later passes run 1-2 % faster as one chain
+// than as digit-group segments plus joint counting, and position segments gain ~1 %
+// in the first pass.
+static int seg_later() {
+    static int v = 2;
+    if (v == 2) {
+        const char *e = std::getenv("LABSORT_SEG");
+        v = !e ? OSP_SEG_LATER : std::strcmp(e, "on") == 0 ? 1 : std::strcmp(e, "none") == 0 ? -1 : 0;
+    }
+    return v;
+}
+
 hipError_t launch_plan8(const uint32_t *hps, size_t n, int in_is_out, Plan *plan, SegPlan *segplans, uint32_t *hist,
                         hipStream_t s) {
-    k_plan8<<<1, 256, 0, s>>>(hps, (uint32_t)n, in_is_out, plan, segplans, hist);
+    k_plan8<<<1, 256, 0, s>>>(hps, (uint32_t)n, in_is_out, seg_later(), plan, segplans, hist);
     return hipGetLastError();
 }
 
 hipError_t launch_segplan(const Plan *plan, int pass, size_t n, const uint32_t *hist, const uint32_t *joint,
                           SegPlan *segplans, hipStream_t s) {
-    k_segplan<<<1, 256, 0, s>>>(plan, pass, (uint32_t)n, hist, joint, segplans);
+    k_segplan<<<1, 256, 0, s>>>(plan, pass, (uint32_t)n, seg_later(), hist, joint, segplans);
     return hipGetLastError();
 }
 

@@ -37,3 +37,14 @@ def test_onesweep_variant(oracle, variant):
     env = dict(os.environ, LABSORT_OSP=variant)
     r = subprocess.run([sys.executable, "-c", SCRIPT, REPO], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("seg", ["first", "on", "none"])
+def test_onesweep_chains(oracle, seg):
+    """Every look-back chain layout (LABSORT_SEG) sorts correctly with the default
+    rank: position segments in the first pass only, digit-group segments in the
+    later passes too (joint histograms), one chain everywhere."""
+    env = dict(os.environ, LABSORT_SEG=seg)
+    env.pop("LABSORT_OSP", None)
+    r = subprocess.run([sys.executable, "-c", SCRIPT, REPO], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
