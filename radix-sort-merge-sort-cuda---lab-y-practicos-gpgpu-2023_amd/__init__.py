@@ -23,7 +23,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblabsort.so")
+# LABSORT_LIBRARY: path of an alternative build (diagnostic builds under harness/exp)
+LIB_PATH = os.environ.get("LABSORT_LIBRARY") or os.path.join(HERE, "liblabsort.so")
 
 OK, ERR_ARG, ERR_HIP, ERR_DEVICE = 0, 1, 2, 3
 ALGO = {"radix": 0, "merge": 1, "radix1": 2}

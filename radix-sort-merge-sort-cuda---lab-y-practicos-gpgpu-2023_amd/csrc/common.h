@@ -16,14 +16,39 @@ constexpr int OS_TILE = OS_BLOCK * OS_KPT;  // 8192 keys per tile
 constexpr int HIST_BLOCK = 1024;
 
 // ---- persistent pipelined onesweep (8-bit digits) ----
-constexpr int OSP_BLOCK = 1024;
-constexpr int OSP_KPT = 16;
+// The OSP_* shape constants can be overridden (-DLABSORT_OSP_BLOCK=... etc.) for
+// diagnostic builds under harness/exp; the shipped library uses the defaults.
+#ifndef LABSORT_OSP_BLOCK
+#define LABSORT_OSP_BLOCK 1024
+#endif
+#ifndef LABSORT_OSP_KPT
+#define LABSORT_OSP_KPT 16
+#endif
+#ifndef LABSORT_OSP_LBW
+#define LABSORT_OSP_LBW 4
+#endif
+#ifndef LABSORT_OSP_LBW2
+#define LABSORT_OSP_LBW2 4
+#endif
+#ifndef LABSORT_OSP_PREFETCH
+#define LABSORT_OSP_PREFETCH 0
+#endif
+#ifndef LABSORT_OSP_NT
+#define LABSORT_OSP_NT 0
+#endif
+#ifndef LABSORT_OSP_BPC
+#define LABSORT_OSP_BPC 1
+#endif
+constexpr int OSP_BLOCK = LABSORT_OSP_BLOCK;
+constexpr int OSP_KPT = LABSORT_OSP_KPT;
 constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 16384 keys per tile
-constexpr int OSP_LBW = 4;                     // look-back window (predecessor tiles per round)
+constexpr int OSP_LBW = LABSORT_OSP_LBW;    // look-back window of the first round (predecessor tiles)
+constexpr int OSP_LBW2 = LABSORT_OSP_LBW2;  // look-back window of the later rounds
+constexpr bool OSP_PREFETCH = LABSORT_OSP_PREFETCH != 0;  // next tile's keys loaded one iteration ahead
 constexpr int OSP_RANK_BALLOT = 0, OSP_RANK_MATCH = 1, OSP_RANK_ATOMIC = 2;  // k_onesweep_p<RANK, HIST_FIRST>
 constexpr int OSP_SEG_LATER = 0;  // 1: digit-group segments after the first active pass (LABSORT_SEG)
 constexpr int OSP_DEFAULT_VARIANT = 4;          // variant = RANK * 2 + HIST_FIRST
-constexpr int OSP_BLOCKS_PER_CU = 1;           // persistent grid = CUs (16-wave workgroups, LDS ~130 KB, 128 VGPRs)
+constexpr int OSP_BLOCKS_PER_CU = LABSORT_OSP_BPC;           // persistent grid = CUs (16-wave workgroups, LDS ~130 KB, 128 VGPRs)
 static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass tiles");
 
 // ---- segmented look-back chains (8-bit radix) ----
@@ -43,9 +68,15 @@ struct SegPlan {
 };
 
 // ---- LDS tile sort (merge path stage 1 / small sorts) ----
-constexpr int TS_BLOCK = 512;
-constexpr int TS_KPT = 16;
-constexpr int TS_TILE = TS_BLOCK * TS_KPT;  // 8192-key sorted runs
+#ifndef LABSORT_TS_BLOCK
+#define LABSORT_TS_BLOCK 512
+#endif
+#ifndef LABSORT_TS_KPT
+#define LABSORT_TS_KPT 16
+#endif
+constexpr int TS_BLOCK = LABSORT_TS_BLOCK;
+constexpr int TS_KPT = LABSORT_TS_KPT;
+constexpr int TS_TILE = TS_BLOCK * TS_KPT;  // sorted run length of the tile sort
 
 // ---- merge path ----
 constexpr int MG_BLOCK = 256;

@@ -652,6 +652,42 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
 // ever waits on tiles whose aggregates are published unconditionally right after
 // their histogram: forward progress holds for any grid size or residency.
 // ---------------------------------------------------------------------------------
+// Phase stamps (diagnostic builds only, -DOSP_STAMPS): each wave sums the shader-clock
+// cycles it spends in each phase of the tile loop and adds them into g_osp_stamps at
+// exit; labsort_exp_stamps reads them.  OSP_T(i, w) closes phase i after waiting for
+// (w & 1) global memory / (w & 2) LDS operations to complete.
+#ifdef OSP_STAMPS
+__device__ unsigned long long g_osp_stamps[16];
+#define OSP_T(i, w)                                                              \
+    do {                                                                         \
+        if ((w) == 1) __builtin_amdgcn_s_waitcnt(0x0F70);                       \
+        if ((w) == 2) __builtin_amdgcn_s_waitcnt(0xC07F);                       \
+        if ((w) == 3) __builtin_amdgcn_s_waitcnt(0);                            \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
+        st_[i] += t_ - tp_;                                                      \
+        tp_ = t_;                                                                \
+    } while (0)
+#define OSP_CNT(x) (x)
+#else
+#define OSP_T(i, w) \
+    do {            \
+    } while (0)
+#define OSP_CNT(x) \
+    do {           \
+    } while (0)
+#endif
+
+// key stream accesses of the onesweep pass (LABSORT_OSP_NT bit 0: nontemporal scatter
+// stores, bit 1: nontemporal key loads)
+__device__ __forceinline__ void osp_store(uint32_t *p, uint32_t v) {
+    if constexpr (LABSORT_OSP_NT & 1) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ uint32_t osp_load(const uint32_t *p) {
+    if constexpr (LABSORT_OSP_NT & 2) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
 template <bool MATCH>
 struct OspSmem {
     static constexpr int R = 256, W = OSP_BLOCK / WAVE, TILE = OSP_TILE;
@@ -666,7 +702,7 @@ struct OspSmem {
     uint32_t tpre[NSEG + 1];
     uint32_t joint[NSEG * R];  // (top nibble of this digit, next active digit) counts
     uint32_t wsum[8];
-    uint32_t next;
+    uint32_t next, next2;
 };
 
 constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
@@ -688,7 +724,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                                                           uint32_t *lookback, uint32_t *counter, uint32_t *err,
                                                           uint32_t *__restrict__ joint) {
     using S = OspSmem<RANK != OSP_RANK_BALLOT>;
-    constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW;
+    constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW, LBW2 = OSP_LBW2;
     static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
     __shared__ S sm;
 
@@ -722,13 +758,20 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             if (l < sp->tpre[sg + 1] - sp->tpre[sg]) return c;
         }
     };
-    if (tid == 0) sm.next = acquire();
+    if (tid == 0) {
+        const uint32_t c0 = acquire();
+        sm.next = c0;
+        sm.next2 = (OSP_PREFETCH && c0 != OSP_DONE) ? acquire() : OSP_DONE;
+    }
     if (RANK == OSP_RANK_ATOMIC && wid == 0) {
         const bool ord = lds_lane_ordered(sm.probe, lane);
         if (lane == 0) sm.ordered = ord ? 1u : 0u;
     }
     __syncthreads();
-    uint32_t cB = sm.next;
+    // OSP_PREFETCH: tile B's keys were loaded one iteration ahead (while the previous
+    // B was ranked and A scattered); the loads of the tile after B (C) are issued at
+    // the top of B's iteration into kN.
+    uint32_t cB = sm.next, cC = sm.next2;
     const bool atomic_rank = RANK == OSP_RANK_ATOMIC && __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
 
     // carried state of tile A (slot = look-back slot, lo = slot of its segment's first tile)
@@ -738,14 +781,45 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     uint32_t aggA = 0, dstartA = 0;
     uint32_t *wh = sm.wh + wid * R;
     uint64_t *wm = sm.match + wid * R;
+#ifdef OSP_STAMPS
+    unsigned long long st_[10] = {}, tp_ = __builtin_amdgcn_s_memtime();
+    unsigned long long lbr_ = 0, lbs_ = 0, lbw_ = 0, lbt_ = 0;  // look-back rounds, stalls, tiles walked, look-backs
+#endif
+    // input range of tile c: [beg, beg + nvalid)
+    auto tile_range = [&](uint32_t c, uint32_t &beg, uint32_t &nvalid) {
+        const uint32_t sg = c & segmask, l = c >> segbits;
+        beg = sm.start[sg] + l * (uint32_t)TILE;
+        const uint32_t end = sm.start[sg + 1];
+        nvalid = (end - beg) < (uint32_t)TILE ? (end - beg) : (uint32_t)TILE;
+    };
+    // keys of tile c in the wave's blocked layout; sentinels (digit 255) past its end
+    auto load_tile = [&](uint32_t c, uint32_t (&k)[KPT]) {
+        uint32_t beg, nv;
+        tile_range(c, beg, nv);
+        const uint32_t woff = wid * (KPT * WAVE) + lane;
+        const uint32_t *src = in + beg + woff;
+        if (nv == (uint32_t)TILE) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) k[j] = osp_load(src + j * WAVE);
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) k[j] = woff + j * WAVE < nv ? osp_load(src + j * WAVE) : sentinel;
+        }
+    };
+    uint32_t kB[KPT], kN[KPT];
+    if (OSP_PREFETCH && cB != OSP_DONE) load_tile(cB, kN);
+
     for (;;) {
+        if (OSP_PREFETCH) {  // B's keys, loaded one iteration ahead
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) kB[j] = kN[j];
+        }
         const bool haveB = cB != OSP_DONE;
         const uint32_t segB = cB & segmask, lB = cB >> segbits;
         const uint32_t loB = haveB ? sm.tpre[segB] : 0u, slotB = loB + lB;
-        const uint32_t begB = haveB ? sm.start[segB] + lB * (uint32_t)TILE : 0u;
-        const uint32_t endB = haveB ? sm.start[segB + 1] : 0u;
-        const uint32_t nvalidB = (endB - begB) < (uint32_t)TILE ? (endB - begB) : (uint32_t)TILE;
-        uint32_t kB[KPT], rB[KPT];
+        uint32_t begB = 0, nvalidB = 0;
+        if (haveB) tile_range(cB, begB, nvalidB);
+        uint32_t rB[KPT / 2];  // wave-local ranks of B, two 16-bit ranks per register
         uint32_t hB = 0, xB = 0;
         // look-back window of A (its latency hides behind B's load, histogram and rank)
         if (slotA != OSP_DONE && tid < (uint32_t)R) {
@@ -754,26 +828,18 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             for (int i = 0; i < LBW; ++i)
                 lwA[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
         }
-        if (haveB) {
-            const uint32_t woff = wid * (KPT * WAVE) + lane;
-            const uint32_t *src = in + begB + woff;
-            if (nvalidB == (uint32_t)TILE) {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) kB[j] = src[j * WAVE];
-                if constexpr (HIST_FIRST) {
-#pragma unroll
-                    for (int j = 0; j < KPT; ++j) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const bool ok = woff + j * WAVE < nvalidB;
-                    kB[j] = ok ? src[j * WAVE] : sentinel;
-                    if constexpr (HIST_FIRST)
-                        if (ok) atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
-                }
-            }
+        if (OSP_PREFETCH) {
+            if (cC != OSP_DONE) load_tile(cC, kN);
+        } else if (haveB) {
+            load_tile(cB, kB);
         }
+        if (HIST_FIRST && haveB) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j)
+                if ((uint32_t)j * WAVE + wid * (KPT * WAVE) + lane < nvalidB)
+                    atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
+        }
+        OSP_T(0, 1);  // look-back issue + B's keys landed
         if constexpr (HIST_FIRST) __syncthreads();  // (1) histogram of B complete
         if (haveB) {
             if (HIST_FIRST && tid < (uint32_t)R) {
@@ -787,56 +853,80 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                 }
                 if (lane == 63) sm.wsum[wid] = xB;
             }
-            // stable wave rank of B: lanes sharing a digit found by an LDS atomic-XOR
+            // stable wave rank of B
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
                 if (atomic_rank) {
-                    rB[j] = (__hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) << 8) | d;
+                    const uint32_t r = __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
                 } else {
                     const uint64_t m = RANK != OSP_RANK_BALLOT ? lds_peers(wm + d, lane) : match8(d);
                     const uint32_t pre = mbcnt64(m);
                     const uint32_t old = wh[d];
                     if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
-                    rB[j] = ((old + pre) << 8) | d;
+                    rB[j / 2] = (j & 1) ? rB[j / 2] | ((old + pre) << 16) : old + pre;
                 }
             }
         }
+        OSP_T(1, 2);  // rank of B
         // complete the look-back of A; publish its inclusive prefix (within its segment)
         if (slotA != OSP_DONE && tid < (uint32_t)R) {
+            // first round: the LBW words loaded at the top of the iteration; later
+            // rounds (each a dependent memory round trip) read LBW2 words at once
             uint32_t excl = 0, spins = 0;
             int32_t hi = (int32_t)slotA - 1;
-            for (;;) {
-                int consumed = 0;
-                bool done = false, stall = false;
+            int consumed = 0;
+            bool done = false, stall = false;
 #pragma unroll
-                for (int i = 0; i < LBW; ++i) {
-                    if (!done && !stall) {
-                        if ((lwA[i] & ~LB_VAL) == 0u) stall = true;
-                        else {
-                            excl += lwA[i] & LB_VAL;
-                            ++consumed;
-                            done = (lwA[i] & LB_INC) != 0u;
-                        }
+            for (int i = 0; i < LBW; ++i) {
+                if (!done && !stall) {
+                    if ((lwA[i] & ~LB_VAL) == 0u) stall = true;
+                    else {
+                        excl += lwA[i] & LB_VAL;
+                        ++consumed;
+                        done = (lwA[i] & LB_INC) != 0u;
                     }
                 }
-                if (done) break;
+            }
+            OSP_CNT(lbw_ += consumed);
+            while (!done) {
+                OSP_CNT(++lbr_);
                 hi -= consumed;
                 if (stall) {
+                    OSP_CNT(++lbs_);
                     if (++spins > SPIN_LIMIT) {
                         atomicOr(err, 1u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
+                uint32_t lw[LBW2];
 #pragma unroll
-                for (int i = 0; i < LBW; ++i)
-                    lwA[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
+                for (int i = 0; i < LBW2; ++i)
+                    lw[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
+                consumed = 0;
+                stall = false;
+#pragma unroll
+                for (int i = 0; i < LBW2; ++i) {
+                    if (!done && !stall) {
+                        if ((lw[i] & ~LB_VAL) == 0u) stall = true;
+                        else {
+                            excl += lw[i] & LB_VAL;
+                            ++consumed;
+                            done = (lw[i] & LB_INC) != 0u;
+                        }
+                    }
+                }
+                OSP_CNT(lbw_ += consumed);
             }
+            OSP_CNT(++lbt_);
             if (slotA > loA) st_agent(lookback + (size_t)slotA * R + tid, LB_INC | (excl + aggA));
             sm.delta[tid] = sp->base[segA * R + tid] + excl - dstartA;
         }
+        OSP_T(2, 3);  // look-back completion of A (waves 0-3)
         __syncthreads();  // (2) delta of A, wave counts and wsum of B
+        OSP_T(3, 0);
         if (!HIST_FIRST && haveB) {
             // tile histogram = sum of the per-wave counts; publish B's aggregate, scan it
             if (tid < (uint32_t)R) {
@@ -860,18 +950,20 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
-                    out[sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i] = kA[j];
+                    osp_store(out + sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i, kA[j]);
                 }
             } else {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
-                    if (i < nvalidA) out[sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i] = kA[j];
+                    if (i < nvalidA) osp_store(out + sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i, kA[j]);
                 }
             }
         }
+        OSP_T(4, 0);  // aggregate of B, scatter of A issued
         if (!haveB) break;
         if constexpr (!HIST_FIRST) __syncthreads();  // (2b) wsum of B
+        OSP_T(5, 0);
         if (tid < (uint32_t)R) {
             uint32_t add = 0;
 #pragma unroll
@@ -888,11 +980,15 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             sm.hist[tid] = 0u;
             dstartA = ds;
         }
-        if (tid == 0) sm.next = acquire();
+        if (tid == 0) sm.next = (!OSP_PREFETCH || cC != OSP_DONE) ? acquire() : OSP_DONE;
+        OSP_T(6, 0);  // wave offsets (waves 0-3), acquisition
         __syncthreads();  // (3) wave offsets of B
+        OSP_T(7, 0);
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) sm.keys[wh[rB[j] & 255u] + (rB[j] >> 8)] = kB[j];
+        for (int j = 0; j < KPT; ++j)
+            sm.keys[wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = kB[j];
         __syncthreads();  // (4) B reordered in LDS
+        OSP_T(8, 0);  // reorder
 #pragma unroll
         for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[j * OSP_BLOCK + tid];
         // each wave clears its own counters (no barrier before the next ranking)
@@ -905,13 +1001,30 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                     atomicAdd(&sm.joint[((x >> (shift + 4)) & 15u) * R + ((x >> nshift) & 255u)], 1u);
             }
         }
+        OSP_T(9, 2);  // readback, joint counts
         slotA = slotB;
         loA = loB;
         segA = segB;
         nvalidA = nvalidB;
         aggA = hB;
-        cB = sm.next;
+        if (OSP_PREFETCH) {
+            cB = cC;
+            cC = sm.next;
+        } else {
+            cB = sm.next;
+        }
     }
+#ifdef OSP_STAMPS
+    if (lane == 0)
+        for (int i = 0; i < 10; ++i) atomicAdd(&g_osp_stamps[i], st_[i]);
+    if (tid == 0) atomicAdd(&g_osp_stamps[10], 1ull);
+    if (tid == 0) {
+        atomicAdd(&g_osp_stamps[11], lbr_);
+        atomicAdd(&g_osp_stamps[12], lbs_);
+        atomicAdd(&g_osp_stamps[13], lbw_);
+        atomicAdd(&g_osp_stamps[14], lbt_);
+    }
+#endif
     if (count_next) {
         __syncthreads();
         uint32_t *j = joint + (size_t)nxt * NSEG * R;
@@ -928,7 +1041,6 @@ struct TsSmem {
     static constexpr int R = 256, W = BLOCK / WAVE, TILE = BLOCK * KPT;
     uint32_t keys[TILE];
     uint32_t whist[W * R];
-    uint64_t match[W * R];
     uint32_t dstart[R];
     uint32_t wsum[W];
     uint32_t red_and[W];
@@ -938,7 +1050,7 @@ struct TsSmem {
 };
 
 template <int BLOCK, int KPT>
-__global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t flip) {
+__global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t flip) {
     using S = TsSmem<BLOCK, KPT>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE;
     __shared__ S sm;
@@ -985,26 +1097,26 @@ __global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_
         diff = aa ^ oo;
     }
     uint32_t *wh = sm.whist + wid * R;
-    uint64_t *wm = sm.match + wid * R;
     for (int pass = 0; pass < 4; ++pass) {
         const uint32_t shift = pass * 8;
         if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the block
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
-        uint32_t dig[KPT], rank[KPT];
+        uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            // stable wave rank: lane-ordered returning atomic, else peers by an LDS atomic-XOR
+            // stable wave rank: lane-ordered returning atomic, else peers by 8 ballots
             const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-            dig[j] = d;
+            uint32_t r;
             if (atomic_rank) {
-                rank[j] = __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                r = __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
             } else {
-                const uint64_t m = lds_peers(wm + d, lane);
+                const uint64_t m = match8(d);
                 const uint32_t pre = mbcnt64(m);
                 const uint32_t old = wh[d];
                 if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
-                rank[j] = old + pre;
+                r = old + pre;
             }
+            rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
         }
         __syncthreads();
         uint32_t tot = 0;
@@ -1020,7 +1132,10 @@ __global__ __launch_bounds__(BLOCK) void k_tile_sort(const uint32_t *in, uint32_
         if (tid < (uint32_t)R) sm.dstart[tid] = ds;
         __syncthreads();
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) sm.keys[sm.dstart[dig[j]] + wh[dig[j]] + rank[j]] = k[j];
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+            sm.keys[sm.dstart[d] + wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = k[j];
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
@@ -1485,3 +1600,14 @@ hipError_t launch_count_descents(const uint32_t *keys, size_t n, uint32_t flip, 
 }
 
 }  // namespace labsort
+
+#ifdef OSP_STAMPS
+extern "C" int labsort_exp_stamps(unsigned long long *host16, int reset) {
+    if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(labsort::g_osp_stamps), 16 * 8) != hipSuccess) return 2;
+    if (reset) {
+        unsigned long long z[16] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(labsort::g_osp_stamps), z, sizeof z) != hipSuccess) return 2;
+    }
+    return 0;
+}
+#endif
