@@ -43,3 +43,7 @@ if [[ "$STEPS" == *dist* ]]; then
     grep '"metric"' "$O/bench_dist2_$ex.log" | cut -c1-400
   done
 fi
+if [[ "$STEPS" == *mprof* ]]; then
+  run rocprof stats merge
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/mprof_$TAG" -o run -- python3 "$R/bench.py" --algo merge --steps 10 --warmup 2 --no-cpu-baseline > "$O/mprof_$TAG.log" 2>&1 || { tail -30 "$O/mprof_$TAG.log"; exit 1; }
+fi

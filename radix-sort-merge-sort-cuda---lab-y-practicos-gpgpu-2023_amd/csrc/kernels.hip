@@ -1061,14 +1061,25 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
 
     uint32_t k[KPT];
     uint32_t a = ~0u, o = 0u;
+    const bool full = base + (uint32_t)TILE <= n;  // no bounds checks (one base address)
+    if (full) {
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-        const uint32_t idx = wbase + j * WAVE;
-        const bool ok = idx < n;
-        k[j] = ok ? in[idx] : sentinel;
-        const uint32_t x = k[j] ^ flip;
-        a &= ok ? x : ~0u;
-        o |= ok ? x : 0u;
+        for (int j = 0; j < KPT; ++j) k[j] = in[wbase + j * WAVE];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            a &= k[j] ^ flip;
+            o |= k[j] ^ flip;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            const bool ok = idx < n;
+            k[j] = ok ? in[idx] : sentinel;
+            const uint32_t x = k[j] ^ flip;
+            a &= ok ? x : ~0u;
+            o |= ok ? x : 0u;
+        }
     }
     // bits on which the tile's keys differ -> passes that are not the identity
 #pragma unroll
@@ -1140,10 +1151,15 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
 #pragma unroll
         for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
     }
+    if (full) {
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-        const uint32_t idx = wbase + j * WAVE;
-        if (idx < n) out[idx] = k[j];
+        for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            if (idx < n) out[idx] = k[j];
+        }
     }
 }
 

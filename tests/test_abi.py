@@ -71,17 +71,18 @@ def test_no_oracle_in_product():
 # ---- host logic (no device calls) ------------------------------------------------------
 def test_sizes_and_limits(ls):
     T = ls.merge_tile_keys()
-    assert ls.tile_keys() == 8192 and T in (1024, 2048, 4096, 8192)
+    TS = ls.tile_keys()
+    assert TS in (8192, 16384, 32768) and T in (1024, 2048, 4096, 8192)
     assert ls.max_keys("radix") == (1 << 30) - 1
     assert ls.max_keys("merge") == 2**31 - 1
     assert ls.merge_parts(0) == 2 and ls.merge_parts(T) == 3 and ls.merge_parts(T + 1) == 4
     for algo in ("radix", "merge", "radix1"):
         prev = 0
-        for n in (1, 100, 8192, 8193, 1 << 20, 1 << 28):
+        for n in (1, 100, TS, TS + 1, 1 << 20, 1 << 28):
             w = ls.workspace_bytes(n, algo)
             assert w >= prev
             prev = w
-            if n > 8192:
+            if n > TS:
                 assert w >= 4 * n  # one ping-pong buffer of n keys
     # radix at 2^28: tmp keys + 4 passes x 32768 tiles x 256 look-back words + hist
     assert ls.workspace_bytes(1 << 28, "radix") < 4 * (1 << 28) + 4 * 32768 * 256 * 4 + (1 << 20)

@@ -86,7 +86,7 @@ def test_histogram(ls, oracle, torch_gpu, bits, key):
 
 
 # ---- whole sorts ----------------------------------------------------------------------------
-SIZES = [1, 2, 63, 64, 65, 1000, 8191, 8192, 8193, 65536, 100_000, (1 << 20) + 12345]
+SIZES = [1, 2, 63, 64, 65, 1000, 8191, 8192, 8193, 32767, 32768, 32769, 65536, 100_000, (1 << 20) + 12345]
 DISTS = ["u32", "u31", "mod100", "mod1000", "sorted", "reversed", "const", "lowbits"]
 
 
