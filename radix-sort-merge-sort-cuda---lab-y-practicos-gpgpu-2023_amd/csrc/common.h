@@ -84,6 +84,11 @@ constexpr int TS_TILE = TS_BLOCK * TS_KPT;  // sorted run length of the tile sor
 constexpr int MG_BLOCK = 256;
 constexpr int MG_KPT = 8;
 constexpr int MG_TILE = MG_BLOCK * MG_KPT;
+constexpr int MG_MAX_TPB = 256;       // most consecutive output tiles per merge workgroup
+#ifndef LABSORT_MG_BRACKET
+#define LABSORT_MG_BRACKET 8
+#endif
+constexpr int MG_BRACKET = LABSORT_MG_BRACKET;  // co-rank search: every 8th tile first, the rest bracketed
 constexpr int MG_BLOCKS_PER_CU = 8;  // persistent merge pass grid  // 4096 outputs per workgroup
 
 constexpr int MAX_PASSES = 32;

@@ -1190,11 +1190,14 @@ __global__ __launch_bounds__(256) void k_wave_split(uint32_t *keys, uint32_t n, 
 // ---------------------------------------------------------------------------------
 __device__ __forceinline__ bool key_le(uint32_t a, uint32_t b, uint32_t flip) { return (a ^ flip) <= (b ^ flip); }
 
-// number of A elements among the first `diag` of merge(A,B), A first on ties
+// number of A elements among the first `diag` of merge(A,B), A first on ties; the
+// answer is searched in [lo, hi] (callers may pass a bracket known from neighbouring
+// diagonals; it is clipped to the feasible range)
 __device__ __forceinline__ uint32_t corank(const uint32_t *A, uint32_t la, const uint32_t *B, uint32_t lb,
-                                           uint32_t diag, uint32_t flip) {
-    uint32_t lo = diag > lb ? diag - lb : 0u;
-    uint32_t hi = diag < la ? diag : la;
+                                           uint32_t diag, uint32_t flip, uint32_t lo = 0u, uint32_t hi = ~0u) {
+    if (diag > lb && lo < diag - lb) lo = diag - lb;
+    if (hi > diag) hi = diag;
+    if (hi > la) hi = la;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
         if (key_le(A[mid], B[diag - 1u - mid], flip)) lo = mid + 1u;
@@ -1259,60 +1262,72 @@ __device__ __forceinline__ PairGeom pair_of(uint32_t o, uint32_t n, uint32_t run
     return g;
 }
 
-// co-rank at the start of every output tile of a merge pass
-__global__ __launch_bounds__(256) void k_merge_part_pass(const uint32_t *__restrict__ src, uint32_t n, uint32_t run,
-                                                         uint32_t flip, uint32_t *__restrict__ part,
-                                                         uint32_t ntiles) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= ntiles) return;
-    const uint32_t o = i * (uint32_t)MG_TILE;
-    const PairGeom g = pair_of(o, n, run);
-    part[i] = corank(src + g.pb, g.la, src + g.pb + g.la, g.lb, o - g.pb, flip);
-}
-
-template <int BLOCK, int KPT>
-__global__ __launch_bounds__(BLOCK) void k_merge_pass(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
-                                                      uint32_t n, uint32_t run, uint32_t flip,
-                                                      const uint32_t *__restrict__ part) {
-    __shared__ MgSmem sm;
-    const uint32_t i = blockIdx.x;
-    const uint32_t o0 = i * (uint32_t)MG_TILE;
-    const uint32_t o1 = (n - o0) < (uint32_t)MG_TILE ? n : o0 + (uint32_t)MG_TILE;
-    const PairGeom g = pair_of(o0, n, run);
-    const uint32_t a0 = part[i];
-    const uint32_t a1 = (o1 - g.pb == g.la + g.lb) ? g.la : part[i + 1];
-    const uint32_t b0 = (o0 - g.pb) - a0, b1 = (o1 - g.pb) - a1;
-    merge_tile<BLOCK, KPT>(src + g.pb, a0, a1, src + g.pb + g.la, b0, b1, dst + o0, flip, sm);
-}
-
-// Persistent, software-pipelined merge pass: workgroup b merges output tiles
-// b, b+G, b+2G, ...; the keys of the next tile are loaded into registers while the
-// current tile is merged in LDS, and the co-ranks two tiles ahead, so the global
-// load latency hides behind the LDS merge instead of stalling every tile.
+// Persistent, software-pipelined merge pass.  Workgroup b merges the consecutive
+// output tiles [b*m, (b+1)*m): it first finds the co-ranks at all their starts with
+// concurrent binary searches (one per thread, their latencies overlapping; no
+// separate partition launch), then merges tile after tile, the keys of the next
+// tile loading into registers while the current one is merged in LDS.
 template <int BLOCK, int KPT>
 __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
-                                                        uint32_t n, uint32_t run, uint32_t flip,
-                                                        const uint32_t *__restrict__ part, uint32_t ntiles) {
+                                                        uint32_t n, uint32_t run, uint32_t flip, uint32_t ntiles,
+                                                        uint32_t m) {
     constexpr uint32_t T = (uint32_t)(BLOCK * KPT);
-    static_assert(T == (uint32_t)MG_TILE, "partition granularity");
+    static_assert(T == (uint32_t)MG_TILE, "tile granularity");
     __shared__ MgSmem sm;
-    const uint32_t tid = threadIdx.x, G = gridDim.x;
+    __shared__ uint32_t s_part[MG_MAX_TPB + 1];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t t0 = blockIdx.x * m;
+    if (t0 >= ntiles) return;
+    const uint32_t t1 = t0 + m < ntiles ? t0 + m : ntiles;
+    // A-side co-rank at the start of every tile of this workgroup (and of the next one),
+    // in two rounds: every MG_BRACKET-th tile over its whole pair of runs, then the
+    // others inside the bracket of their round-1 neighbours (co-ranks are monotone
+    // within a pair and move by at most one per output key), which keeps the second
+    // round's probes in a few cached lines instead of the whole run.  (A third level
+    // measured slower: each level adds a chain of dependent loads.)
+    const uint32_t nb = t1 - t0;
+    // co-rank of tile i, bracketed by the tiles il = i - i % S and min(il + S, nb) when S > 0
+    auto search = [&](uint32_t i, uint32_t S) {
+        const uint32_t o = (t0 + i) * T;
+        if (o >= n) return 0u;
+        const PairGeom g = pair_of(o, n, run);
+        uint32_t lo = 0u, hi = ~0u;
+        if (S) {
+            const uint32_t il = i - i % S, ih = il + S < nb ? il + S : nb;
+            const uint32_t ol = (t0 + il) * T, oh = (t0 + ih) * T;
+            if (pair_of(ol, n, run).pb == g.pb) {
+                lo = s_part[il];
+                hi = lo + (o - ol);
+            }
+            if (oh < n && pair_of(oh, n, run).pb == g.pb) {
+                const uint32_t ah = s_part[ih];
+                hi = hi < ah ? hi : ah;
+                if (ah > oh - o && lo < ah - (oh - o)) lo = ah - (oh - o);
+            }
+        }
+        return corank(src + g.pb, g.la, src + g.pb + g.la, g.lb, o - g.pb, flip, lo, hi);
+    };
+    for (uint32_t i = tid * MG_BRACKET; i <= nb; i += BLOCK * MG_BRACKET) s_part[i] = search(i, 0);
+    if (tid == 0 && nb % MG_BRACKET) s_part[nb] = search(nb, 0);
+    __syncthreads();
+    for (uint32_t i = tid; i < nb; i += BLOCK)
+        if (i % MG_BRACKET) s_part[i] = search(i, MG_BRACKET);
+    __syncthreads();
     struct Geo {
         uint32_t o0, tot, la, sa, sb;  // output start, keys, A keys, A start, B start (absolute)
     };
-    auto geo = [&](uint32_t t, uint32_t p0, uint32_t p1) {
+    auto geo = [&](uint32_t t) {
         Geo q;
         q.o0 = t * T;
         const uint32_t o1 = (n - q.o0) < T ? n : q.o0 + T;
         const PairGeom g = pair_of(q.o0, n, run);
-        const uint32_t a0 = p0;
-        const uint32_t a1 = (o1 - g.pb == g.la + g.lb) ? g.la : p1;
-        const uint32_t b0 = (q.o0 - g.pb) - a0, b1 = (o1 - g.pb) - a1;
+        const uint32_t a0 = s_part[t - t0];
+        const uint32_t a1 = (o1 - g.pb == g.la + g.lb) ? g.la : s_part[t + 1 - t0];
+        const uint32_t b0 = (q.o0 - g.pb) - a0;
         q.tot = o1 - q.o0;
         q.la = a1 - a0;
         q.sa = g.pb + a0;
         q.sb = g.pb + g.la + b0;
-        (void)b1;
         return q;
     };
     auto load = [&](const Geo &q, uint32_t (&v)[KPT]) {
@@ -1322,26 +1337,18 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
             v[j] = k < q.tot ? src[k < q.la ? q.sa + k : q.sb + (k - q.la)] : 0u;
         }
     };
-    uint32_t t = blockIdx.x;
-    if (t >= ntiles) return;
     uint32_t nx[KPT];
-    Geo cur = geo(t, part[t], part[t + 1]);
+    Geo cur = geo(t0);
     load(cur, nx);
-    uint32_t t2 = t + G;  // co-ranks of the tile after this one
-    uint32_t q0 = t2 < ntiles ? part[t2] : 0u, q1 = t2 < ntiles ? part[t2 + 1] : 0u;
-    for (; t < ntiles; t += G) {
+    for (uint32_t t = t0; t < t1; ++t) {
         __syncthreads();  // previous tile's merge no longer reads sm.in
 #pragma unroll
         for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
-        // next tile: geometry from the prefetched co-ranks, keys into registers
-        const uint32_t tn = t + G;
+        // next tile: geometry from the co-ranks, keys into registers
         Geo nxt = cur;
-        if (tn < ntiles) {
-            nxt = geo(tn, q0, q1);
+        if (t + 1 < t1) {
+            nxt = geo(t + 1);
             load(nxt, nx);
-            const uint32_t t3 = tn + G;
-            q0 = t3 < ntiles ? part[t3] : 0u;
-            q1 = t3 < ntiles ? part[t3 + 1] : 0u;
         }
         __syncthreads();  // sm.in holds the current tile
         const uint32_t la = cur.la, lb = cur.tot - cur.la, tot = cur.tot;
@@ -1579,14 +1586,13 @@ hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStr
 hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t run, uint32_t flip,
                              uint32_t *part, hipStream_t s) {
     if (n == 0) return hipSuccess;
+    (void)part;  // co-ranks are found inside k_merge_pass_p
     const uint32_t ntiles = (uint32_t)((n + MG_TILE - 1) / MG_TILE);
-    k_merge_part_pass<<<(ntiles + 255) / 256, 256, 0, s>>>(in, (uint32_t)n, (uint32_t)run, flip, part, ntiles);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    const unsigned want = (unsigned)(MG_BLOCKS_PER_CU * cu_count());
-    k_merge_pass_p<MG_BLOCK, MG_KPT><<<ntiles < want ? ntiles : want, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n,
-                                                                                        (uint32_t)run, flip, part,
-                                                                                        ntiles);
+    const uint32_t want = (uint32_t)(MG_BLOCKS_PER_CU * cu_count());
+    uint32_t m = (ntiles + want - 1) / want;  // consecutive tiles per workgroup
+    if (m > (uint32_t)MG_MAX_TPB) m = MG_MAX_TPB;
+    const uint32_t g = (ntiles + m - 1) / m;
+    k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m);
     return hipGetLastError();
 }
 
