@@ -106,11 +106,11 @@ RadixLayout radix_layout(size_t n, int bits) {
     L.off_hist = o;
     o += (size_t)L.P * L.R * 4;
     L.off_hps = o;
-    if (bits == 8) o += (size_t)NSEG * 4 * 256 * 4;
+    if (bits == 8) o += (size_t)NSEG * 256 * 4;
     L.off_joint = o;
     if (bits == 8) o += (size_t)4 * NSEG * 256 * 4;
     L.off_counter = o;
-    o += (size_t)L.P * 4;
+    o += (size_t)L.P * OSP_NCTR * 4;
     L.off_err = o;
     o += 16;
     o = align_up(o, 256);
@@ -162,15 +162,15 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
         SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
         {
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
-            HIP_TRY(launch_hist_seg(in, n, flip, hps, s));
+            HIP_TRY(launch_hist_seg(in, n, flip, hps, joint, s));
         }
         HIP_TRY(hipMemsetAsync(ws + L.off_lookback, 0, L.off_hist + L.zero_bytes - L.off_lookback, s));
-        HIP_TRY(launch_plan8(hps, n, in == out ? 1 : 0, plan, sps, hist, s));
+        HIP_TRY(launch_plan8(hps, joint, n, in == out ? 1 : 0, plan, sps, hist, s));
         for (int p = 0; p < L.P; ++p) {
             if (p > 0) HIP_TRY(launch_segplan(plan, p, n, hist, joint, sps, s));
             TimingScope ts(LABSORT_K_ONESWEEP, s);
             HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
-                                      counters + p, err, joint, s));
+                                      counters + (size_t)p * OSP_NCTR, err, s));
         }
     } else {
         HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.zero_bytes, s));
@@ -182,7 +182,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
         for (int p = 0; p < L.P; ++p) {
             TimingScope ts(LABSORT_K_ONESWEEP, s);
             HIP_TRY(launch_onesweep(b, plan, p, bits, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
-                                    counters + p, err, s));
+                                    counters + (size_t)p * OSP_NCTR, err, s));
         }
     }
     HIP_TRY(launch_final_copy(b, plan, n, s));

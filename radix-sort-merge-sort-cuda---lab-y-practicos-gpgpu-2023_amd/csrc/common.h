@@ -36,6 +36,9 @@ constexpr int HIST_BLOCK = 1024;
 #ifndef LABSORT_OSP_NT
 #define LABSORT_OSP_NT 0
 #endif
+#ifndef LABSORT_OSP_XCD
+#define LABSORT_OSP_XCD 1
+#endif
 #ifndef LABSORT_OSP_BPC
 #define LABSORT_OSP_BPC 1
 #endif
@@ -46,8 +49,14 @@ constexpr int OSP_LBW = LABSORT_OSP_LBW;    // look-back window of the first rou
 constexpr int OSP_LBW2 = LABSORT_OSP_LBW2;  // look-back window of the later rounds
 constexpr bool OSP_PREFETCH = LABSORT_OSP_PREFETCH != 0;  // next tile's keys loaded one iteration ahead
 constexpr int OSP_RANK_BALLOT = 0, OSP_RANK_MATCH = 1, OSP_RANK_ATOMIC = 2;  // k_onesweep_p<RANK, HIST_FIRST>
-constexpr int OSP_SEG_LATER = 0;  // 1: digit-group segments after the first active pass (LABSORT_SEG)
+constexpr int OSP_SEG_LATER = 1;  // 1: digit-group segments after the first active pass (LABSORT_SEG)
 constexpr int OSP_DEFAULT_VARIANT = 4;          // variant = RANK * 2 + HIST_FIRST
+// Tile acquisition: OSP_NCTR counters per pass.  With OSP_XCD each XCD (HW_REG_XCC_ID)
+// first takes the tiles of its own segments {x, x + 8} in order, then helps the
+// others; consecutive tiles of a segment then write their shared run-boundary lines
+// through one L2 (harness/exp/bw_probe.hip: abutting 64-key runs 0.67 -> 0.58 ms).
+constexpr bool OSP_XCD = LABSORT_OSP_XCD != 0;
+constexpr int OSP_NCTR = 8;
 constexpr int OSP_BLOCKS_PER_CU = LABSORT_OSP_BPC;           // persistent grid = CUs (16-wave workgroups, LDS ~130 KB, 128 VGPRs)
 static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass tiles");
 
@@ -57,6 +66,8 @@ static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass til
 // upfront histogram kernel computes (see k_hist_seg / k_plan8).
 constexpr int NSEG = 16;
 constexpr int HS_BPS = 16;  // histogram workgroups per position segment
+// first position of segment s of an n-key pass input (first active pass)
+__host__ __device__ inline uint32_t seg_start(uint32_t s, size_t n) { return (uint32_t)((size_t)s * n / NSEG); }
 struct SegPlan {
     uint32_t start[NSEG + 1];  // segment s = pass input positions [start[s], start[s+1])
     uint32_t tpre[NSEG + 1];   // tiles in segments < s = look-back slot of segment s's first tile
@@ -128,13 +139,14 @@ hipError_t launch_plan(const uint32_t *hist, size_t n, int bits, int in_is_out, 
 hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t n, uint32_t flip,
                            const uint32_t *hist, uint32_t *lookback, uint32_t *counter, uint32_t *err,
                            hipStream_t s);
-hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, hipStream_t s);
-hipError_t launch_plan8(const uint32_t *hps, size_t n, int in_is_out, Plan *plan, SegPlan *segplans, uint32_t *hist,
-                        hipStream_t s);
+hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, uint32_t *joint,
+                           hipStream_t s);
+hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, int in_is_out, Plan *plan,
+                        SegPlan *segplans, uint32_t *hist, hipStream_t s);
 hipError_t launch_segplan(const Plan *plan, int pass, size_t n, const uint32_t *hist, const uint32_t *joint,
                           SegPlan *segplans, hipStream_t s);
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
-                             uint32_t *lookback, uint32_t *counter, uint32_t *err, uint32_t *joint, hipStream_t s);
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s);
 hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);

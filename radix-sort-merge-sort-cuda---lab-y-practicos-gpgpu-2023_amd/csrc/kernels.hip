@@ -280,27 +280,35 @@ __global__ __launch_bounds__(256) void k_plan(const uint32_t *__restrict__ hist,
 // the pass starts:
 //   * first active pass: the input is split into NSEG equal position ranges and
 //     k_hist_seg (the upfront histogram, workgroups aligned to the ranges) gives
-//     each range's digit histograms: hps[s][p][d];
+//     each range's digit-0 histogram hps[s][d] (if digit 0 is trivial, the first
+//     active pass runs as one chain);
 //   * later passes: after a pass on digit p the data is ordered (stably) by digit
 //     p, so the keys whose digit p has top nibble g form one contiguous range of the
-//     next active pass's input.  The pass on digit p counts, per key, (top nibble of
-//     digit p, next active digit) into joint[q][g][d] as it histograms each tile,
-//     and k_segplan turns that into the next pass's segments and bases.
+//     next pass's input (digit p + 1).  That segment's digit-(p+1) histogram is the
+//     joint count of (top nibble of digit p, digit p + 1) = a histogram of the 12-bit
+//     key field [8p + 4, 8p + 16): a property of the key multiset, so k_hist_seg
+//     counts it for p = 0, 1, 2 in the same read of the keys, into joint[p+1][g][d].
+//     Digit histograms of passes 1-3 are its marginals.
+//     (A pass whose previous active digit is not p - 1 runs as one chain.)
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restrict__ keys, size_t n, uint32_t flip,
-                                                         uint32_t *__restrict__ hps) {
-    constexpr int SL = 32;  // replicated counters: the 32 lanes of a ds_add group hit 32 banks
-    __shared__ uint32_t h[4 * 256 * SL];
-    for (int i = threadIdx.x; i < 4 * 256 * SL; i += HIST_BLOCK) h[i] = 0u;
+                                                         uint32_t *__restrict__ hps, uint32_t *__restrict__ joint) {
+    constexpr int SL = 32;  // replicated digit-0 counters: the 32 lanes of a ds_add group hit 32 banks
+    constexpr int JF = 4096;  // 12-bit joint fields per pass
+    __shared__ uint32_t h[256 * SL];
+    __shared__ uint32_t hj[3 * JF];
+    for (int i = threadIdx.x; i < 256 * SL; i += HIST_BLOCK) h[i] = 0u;
+    for (int i = threadIdx.x; i < 3 * JF; i += HIST_BLOCK) hj[i] = 0u;
     __syncthreads();
     const uint32_t slot = threadIdx.x & (SL - 1);
     auto count = [&](uint32_t k) {
         k ^= flip;
+        atomicAdd(&h[(k & 255u) * SL + slot], 1u);
 #pragma unroll
-        for (int p = 0; p < 4; ++p) atomicAdd(&h[(p * 256 + ((k >> (8 * p)) & 255u)) * SL + slot], 1u);
+        for (int p = 0; p < 3; ++p) atomicAdd(&hj[p * JF + ((k >> (8 * p + 4)) & (JF - 1))], 1u);
     };
     const uint32_t seg = blockIdx.x / HS_BPS, part = blockIdx.x % HS_BPS;
-    const size_t sb = (size_t)seg * n / NSEG, se = (size_t)(seg + 1) * n / NSEG;
+    const size_t sb = seg_start(seg, n), se = seg_start(seg + 1, n);
     const size_t per = (se - sb + HS_BPS - 1) / HS_BPS;
     const size_t beg = sb + (size_t)part * per < se ? sb + (size_t)part * per : se;
     const size_t end = beg + per < se ? beg + per : se;
@@ -330,11 +338,17 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
         for (size_t t = beg + threadIdx.x; t < end; t += HIST_BLOCK) count(keys[t]);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 4 * 256; i += HIST_BLOCK) {
-        uint32_t s = 0;
+    for (int i = threadIdx.x; i < 256; i += HIST_BLOCK) {
+        uint32_t c = 0;
 #pragma unroll 8
-        for (int q = 0; q < SL; ++q) s += h[i * SL + ((q + i) & (SL - 1))];
-        if (s) atomicAdd(&hps[seg * 1024 + i], s);
+        for (int q = 0; q < SL; ++q) c += h[i * SL + ((q + i) & (SL - 1))];
+        if (c) atomicAdd(&hps[seg * 256 + i], c);
+    }
+    // field f = (digit p+1) << 4 | (top nibble of digit p) -> joint[p+1][nibble][digit]
+    for (int i = threadIdx.x; i < 3 * JF; i += HIST_BLOCK) {
+        const uint32_t c = hj[i];
+        const uint32_t p = (uint32_t)i / JF, f = (uint32_t)i % JF;
+        if (c) atomicAdd(&joint[((p + 1) * NSEG + (f & 15u)) * 256 + (f >> 4)], c);
     }
 }
 
@@ -371,7 +385,9 @@ __device__ void build_segplan(SegPlan *__restrict__ sp, const uint32_t *__restri
         for (int s = 0; s <= NSEG; ++s) {
             sp->tpre[s] = tp;
             if (s < NSEG) {
-                const uint32_t ts = (start[s + 1] - start[s] + OSP_TILE - 1) / OSP_TILE;
+                // tiles aligned to OSP_TILE boundaries (k_onesweep_p's tile_range)
+                const uint32_t a0 = start[s] & ~((uint32_t)OSP_TILE - 1u);
+                const uint32_t ts = start[s + 1] > start[s] ? (start[s + 1] - a0 + OSP_TILE - 1) / OSP_TILE : 0u;
                 tp += ts;
                 mx = ts > mx ? ts : mx;
             }
@@ -384,9 +400,9 @@ __device__ void build_segplan(SegPlan *__restrict__ sp, const uint32_t *__restri
 
 // Pass plan for the 8-bit radix (as k_plan: totals, trivial passes, ping-pong
 // buffers; plus each pass's next active digit) and the first active pass's SegPlan.
-__global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps, uint32_t n, int in_is_out,
-                                               int seg_later, Plan *__restrict__ plan, SegPlan *__restrict__ sps,
-                                               uint32_t *__restrict__ hist_out) {
+__global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps, const uint32_t *__restrict__ joint,
+                                               uint32_t n, int in_is_out, int seg_later, Plan *__restrict__ plan,
+                                               SegPlan *__restrict__ sps, uint32_t *__restrict__ hist_out) {
     __shared__ uint32_t hist[4 * 256];
     __shared__ uint32_t sh[NSEG * 256 + 8];
     __shared__ uint32_t triv[4];
@@ -396,16 +412,18 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
     if (t < 4) triv[t] = 0;
     __syncthreads();
     uint32_t v[4] = {0, 0, 0, 0};
-    for (int s = 0; s < NSEG; ++s)
+    for (int s = 0; s < NSEG; ++s) {
+        v[0] += hps[s * 256 + t];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) v[p] += hps[s * 1024 + p * 256 + t];
+        for (int p = 1; p < 4; ++p) v[p] += joint[(p * NSEG + s) * 256 + t];  // marginal over the nibble
+    }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         hist[p * 256 + t] = v[p];
         hist_out[p * 256 + t] = v[p];
         if (v[p] == n) triv[p] = 1;
     }
-    if (t <= (uint32_t)NSEG) start[t] = seg_later < 0 ? (t ? n : 0u) : (uint32_t)((size_t)t * n / NSEG);
+    if (t <= (uint32_t)NSEG) start[t] = seg_later < 0 ? (t ? n : 0u) : seg_start(t, n);
     __syncthreads();
     if (t == 0) {
         int act[4];
@@ -414,11 +432,11 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
             plan->src[p] = SEL_SKIP;
             plan->dst[p] = SEL_SKIP;
             plan->next[p] = NEXT_NONE;
+            plan->prev[p] = NEXT_NONE;
         }
         for (int p = 0; p < 4; ++p)
             if (!triv[p]) act[k++] = p;
-        if (seg_later > 0)
-            for (int i = 0; i + 1 < k; ++i) plan->next[act[i]] = (uint32_t)act[i + 1];
+        for (int i = 0; i + 1 < k; ++i) plan->next[act[i]] = (uint32_t)act[i + 1];
         plan->active = (uint32_t)k;
         first = k ? act[0] : -1;
         if (k == 0) {
@@ -444,21 +462,22 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
     }
     __syncthreads();
     if (first < 0) return;
-    // first active pass: position segments; hs[s][d] = hps[s][first][d]
-    if (seg_later < 0) {  // one chain
+    // first active pass: position segments when it is digit 0 (hps), else one chain
+    if (seg_later < 0 || first != 0) {
+        if (t <= (uint32_t)NSEG) start[t] = t ? n : 0u;
         for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[first * 256 + t];
         __syncthreads();
         build_segplan(sps + first, sh, start, 2u, sh);
         return;
     }
-    for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = hps[s * 1024 + first * 256 + t];
+    for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = hps[s * 256 + t];
     __syncthreads();
     build_segplan(sps + first, sh, start, 0u, sh);
 }
 
 // SegPlan of pass q when q is active and not the first: segments = ranges of the
-// previous active digit's top nibble (starts from its histogram), histograms from
-// the joint counts the previous pass wrote.
+// previous digit's top nibble (starts from its histogram), histograms = the joint
+// counts k_hist_seg wrote; one chain when the previous active digit is not q - 1.
 __global__ __launch_bounds__(256) void k_segplan(const Plan *__restrict__ plan, int q, uint32_t n, int seg_later,
                                                  const uint32_t *__restrict__ hist, const uint32_t *__restrict__ joint,
                                                  SegPlan *__restrict__ sps) {
@@ -467,7 +486,7 @@ __global__ __launch_bounds__(256) void k_segplan(const Plan *__restrict__ plan, 
     const uint32_t prev = plan->prev[q];
     if (plan->src[q] == SEL_SKIP || prev == NEXT_NONE) return;
     const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
-    if (seg_later <= 0) {  // one chain over the whole input
+    if (seg_later <= 0 || prev + 1u != (uint32_t)q) {  // one chain over the whole input
         for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[q * 256 + t];
         if (t <= (uint32_t)NSEG) start[t] = t ? n : 0u;
         __syncthreads();
@@ -700,7 +719,6 @@ struct OspSmem {
     uint32_t delta[R];
     uint32_t start[NSEG + 1];
     uint32_t tpre[NSEG + 1];
-    uint32_t joint[NSEG * R];  // (top nibble of this digit, next active digit) counts
     uint32_t wsum[8];
     uint32_t next, next2;
 };
@@ -721,8 +739,7 @@ constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 template <int RANK, bool HIST_FIRST>
 __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
                                                           uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
-                                                          uint32_t *lookback, uint32_t *counter, uint32_t *err,
-                                                          uint32_t *__restrict__ joint) {
+                                                          uint32_t *lookback, uint32_t *counter, uint32_t *err) {
     using S = OspSmem<RANK != OSP_RANK_BALLOT>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW, LBW2 = OSP_LBW2;
     static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
@@ -735,14 +752,16 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t shift = (uint32_t)pass * 8u;
     const uint32_t sentinel = ~flip;  // digit 255 in every pass: ranks after all real keys
-    const uint32_t segbits = sp->segbits, segmask = (1u << segbits) - 1u;
-    const uint32_t climit = sp->maxt << segbits;
-    const uint32_t nxt = plan->next[pass];
-    const bool count_next = nxt != NEXT_NONE;
-    const uint32_t nshift = count_next ? nxt * 8u : 0u;
+    // tile id = l * NSEG + segment (tile l of the segment)
+    constexpr uint32_t segbits = 4, segmask = NSEG - 1;
+    // counter groups: G groups of NSEG / G segments, group g = segments {g, g + G, ...};
+    // one group when there is a single chain (mode 2)
+    const bool grouped = OSP_XCD && sp->mode != 2u;
+    const uint32_t gbits = grouped ? 3u : 0u, G = 1u << gbits;
+    const uint32_t lbits = sp->segbits - gbits, lmask = (1u << lbits) - 1u;
+    const uint32_t climit = sp->maxt << lbits;
 
     for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) sm.wh[i] = 0u;
-    for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += OSP_BLOCK) sm.joint[i] = 0u;
     if (tid <= (uint32_t)NSEG) {
         sm.start[tid] = sp->start[tid];
         sm.tpre[tid] = sp->tpre[tid];
@@ -750,13 +769,22 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     if (tid < (uint32_t)R) sm.hist[tid] = 0u;
     // tile acquisition: c -> segment c & 15, tile c >> 4 of that segment; ids past a
     // segment's last tile are skipped, so every segment's tiles are acquired in order
+    // (tid 0 only) own group first, then the others in turn; a group's counter hands out
+    // its segments' tiles in order, whoever takes them
+    const uint32_t home = grouped ? (__builtin_amdgcn_s_getreg((3 << 11) | 20) & (G - 1u)) : 0u;  // HW_REG_XCC_ID
+    uint32_t gk = 0;
     auto acquire = [&]() {
-        for (;;) {
-            const uint32_t c = atomicAdd(counter, 1u);
-            if (c >= climit) return OSP_DONE;
-            const uint32_t sg = c & segmask, l = c >> segbits;
-            if (l < sp->tpre[sg + 1] - sp->tpre[sg]) return c;
+        while (gk < G) {
+            const uint32_t grp = (home + gk) & (G - 1u);
+            const uint32_t c = atomicAdd(counter + grp, 1u);
+            if (c >= climit) {
+                ++gk;
+                continue;
+            }
+            const uint32_t sg = grp | ((c & lmask) << gbits), l = c >> lbits;
+            if (l < sp->tpre[sg + 1] - sp->tpre[sg]) return l * NSEG + sg;
         }
+        return OSP_DONE;
     };
     if (tid == 0) {
         const uint32_t c0 = acquire();
@@ -786,11 +814,14 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     unsigned long long lbr_ = 0, lbs_ = 0, lbw_ = 0, lbt_ = 0;  // look-back rounds, stalls, tiles walked, look-backs
 #endif
     // input range of tile c: [beg, beg + nvalid)
+    // Tiles are aligned to TILE-key boundaries of the input (coalesced, line-aligned
+    // wave loads): a segment's first tile runs from its start to the next boundary.
     auto tile_range = [&](uint32_t c, uint32_t &beg, uint32_t &nvalid) {
         const uint32_t sg = c & segmask, l = c >> segbits;
-        beg = sm.start[sg] + l * (uint32_t)TILE;
-        const uint32_t end = sm.start[sg + 1];
-        nvalid = (end - beg) < (uint32_t)TILE ? (end - beg) : (uint32_t)TILE;
+        const uint32_t s0 = sm.start[sg], a0 = s0 & ~((uint32_t)TILE - 1u);
+        beg = l ? a0 + l * (uint32_t)TILE : s0;
+        const uint32_t tend = a0 + (l + 1u) * (uint32_t)TILE, send = sm.start[sg + 1];
+        nvalid = (tend < send ? tend : send) - beg;
     };
     // keys of tile c in the wave's blocked layout; sentinels (digit 255) past its end
     auto load_tile = [&](uint32_t c, uint32_t (&k)[KPT]) {
@@ -993,15 +1024,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[j * OSP_BLOCK + tid];
         // each wave clears its own counters (no barrier before the next ranking)
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
-        if (count_next) {  // (top nibble of this digit, next active digit) of B's valid keys
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t x = kA[j] ^ flip;
-                if ((uint32_t)j * OSP_BLOCK + tid < nvalidB)
-                    atomicAdd(&sm.joint[((x >> (shift + 4)) & 15u) * R + ((x >> nshift) & 255u)], 1u);
-            }
-        }
-        OSP_T(9, 2);  // readback, joint counts
+        OSP_T(9, 2);  // readback
         slotA = slotB;
         loA = loB;
         segA = segB;
@@ -1025,12 +1048,6 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         atomicAdd(&g_osp_stamps[14], lbt_);
     }
 #endif
-    if (count_next) {
-        __syncthreads();
-        uint32_t *j = joint + (size_t)nxt * NSEG * R;
-        for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += OSP_BLOCK)
-            if (sm.joint[i]) atomicAdd(&j[i], sm.joint[i]);
-    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1508,7 +1525,7 @@ static int cu_count() {
 }
 
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
-                             uint32_t *lookback, uint32_t *counter, uint32_t *err, uint32_t *joint, hipStream_t s) {
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s) {
     const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE + NSEG;
     const size_t want = (size_t)OSP_BLOCKS_PER_CU * cu_count();
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
@@ -1518,20 +1535,21 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
         variant = (e && e[0] >= '0' && e[0] <= '2' && e[1]) ? ((e[0] - '0') << 1) | (e[1] == '1') : OSP_DEFAULT_VARIANT;
     }
     switch (variant) {
-    case 0: k_onesweep_p<0, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
-    case 1: k_onesweep_p<0, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
-    case 2: k_onesweep_p<1, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
-    case 3: k_onesweep_p<1, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
-    case 4: k_onesweep_p<2, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
-    case 5: k_onesweep_p<2, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, joint); break;
+    case 0: k_onesweep_p<0, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
+    case 1: k_onesweep_p<0, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
+    case 2: k_onesweep_p<1, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
+    case 3: k_onesweep_p<1, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
+    case 4: k_onesweep_p<2, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
+    case 5: k_onesweep_p<2, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
 }
 
-hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, hipStream_t s) {
+hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, uint32_t *joint,
+                           hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_hist_seg<<<NSEG * HS_BPS, HIST_BLOCK, 0, s>>>(keys, n, flip, hps);
+    k_hist_seg<<<NSEG * HS_BPS, HIST_BLOCK, 0, s>>>(keys, n, flip, hps, joint);
     return hipGetLastError();
 }
 
@@ -1552,9 +1570,9 @@ static int seg_later() {
     return v;
 }
 
-hipError_t launch_plan8(const uint32_t *hps, size_t n, int in_is_out, Plan *plan, SegPlan *segplans, uint32_t *hist,
-                        hipStream_t s) {
-    k_plan8<<<1, 256, 0, s>>>(hps, (uint32_t)n, in_is_out, seg_later(), plan, segplans, hist);
+hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, int in_is_out, Plan *plan,
+                        SegPlan *segplans, uint32_t *hist, hipStream_t s) {
+    k_plan8<<<1, 256, 0, s>>>(hps, joint, (uint32_t)n, in_is_out, seg_later(), plan, segplans, hist);
     return hipGetLastError();
 }
 
