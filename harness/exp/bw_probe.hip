@@ -34,6 +34,21 @@ __global__ __launch_bounds__(1024) void k_copy_tile(const uint32_t *a, uint32_t 
         for (int j = 0; j < 16; ++j) d[j * 64] = k[j];
     }
 }
+// copy-tile with the destination shifted by SH words: every wave store straddles
+// granules (partial granules written by two stores of one workgroup, not across tiles)
+template <int SH>
+__global__ __launch_bounds__(1024) void k_copy_tile_sh(const uint32_t *a, uint32_t *b, uint32_t ntiles) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const uint32_t *s = a + (size_t)t * 16384 + wid * 1024 + lane;
+        uint32_t k[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) k[j] = s[j * 64];
+        uint32_t *d = b + SH + (size_t)t * 16384 + wid * 1024 + lane;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) d[j * 64] = k[j];
+    }
+}
 __global__ __launch_bounds__(256) void k_read(const uint4 *a, size_t n4, uint32_t *sink) {
     uint32_t x = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
@@ -53,7 +68,9 @@ __global__ __launch_bounds__(256) void k_write(uint4 *b, size_t n4) {
 // contiguous eighth of the tiles, so consecutive tiles share one L2
 // SEL: stores whose 64-B granule lies inside the run are nontemporal, the run's edge
 // granules (shared with the neighbouring tiles) use the default policy
-template <int RUN, int SH, int XL = 0, int NTL = 0, int SEL = 0>
+// HO: handoff pattern -- each tile's run shifted down to the granule boundary, so every
+// tile writes whole granules (its tail granule's words are written by the next tile)
+template <int RUN, int SH, int XL = 0, int NTL = 0, int SEL = 0, int HO = 0>
 __global__ __launch_bounds__(1024) void k_abut(const uint32_t *a, uint32_t *b, uint32_t ntiles) {
     const uint32_t tid = threadIdx.x;
     const size_t stride = (size_t)ntiles * RUN + 64;
@@ -68,10 +85,42 @@ __global__ __launch_bounds__(1024) void k_abut(const uint32_t *a, uint32_t *b, u
         for (int j = 0; j < 16; ++j) {
             const uint32_t i = j * 1024 + tid, d = i / RUN;
             const uint32_t sh = SH == 1 ? (d * 5u + 3u) & 31u : SH == 2 ? ((d * 5u + 3u) & 1u) * 16u : 0u;
-            const size_t rs = d * stride + sh + (size_t)t * RUN, pos = rs + (i % RUN);
+            const size_t rs = d * stride + sh + (size_t)t * RUN, pos = rs + (i % RUN) - (HO ? (rs & 15) : 0);
             const size_t gs = pos & ~(size_t)15;
             if (SEL && gs >= rs && gs + 16 <= rs + RUN) __builtin_nontemporal_store(k[j], b + pos);
             else b[pos] = k[j];
+        }
+    }
+}
+// abutting misaligned runs (as k_abut<RUN, 1, XL>) with each granule shared by two
+// tiles written once, whole, by the earlier tile (a carry handoff's store pattern):
+// the head granule is skipped, the tail granule written as 4 x uint4
+template <int RUN, int XL>
+__global__ __launch_bounds__(1024) void k_abut_own(const uint32_t *a, uint32_t *b, uint32_t ntiles) {
+    const uint32_t tid = threadIdx.x;
+    const size_t stride = (size_t)ntiles * RUN + 64;
+    const uint32_t g = blockIdx.x & 7u, per = ntiles / 8u;
+    for (uint32_t q = XL ? blockIdx.x >> 3 : blockIdx.x; q < (XL ? per : ntiles); q += XL ? gridDim.x >> 3 : gridDim.x) {
+        const uint32_t t = XL ? g * per + q : q;
+        uint32_t k[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) k[j] = a[(size_t)t * 16384 + j * 1024 + tid];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t i = j * 1024 + tid, d = i / RUN;
+            const uint32_t sh = (d * 5u + 3u) & 31u;
+            const size_t rs = d * stride + sh + (size_t)t * RUN, pos = rs + (i % RUN);
+            const size_t gs = pos & ~(size_t)15;
+            if (t > 0 && gs < rs) continue;
+            if (t + 1 < ntiles && gs + 16 > rs + RUN) {
+                if (pos == (gs > rs ? gs : rs)) {
+                    uint4 *p4 = reinterpret_cast<uint4 *>(b + gs);
+                    const uint4 v = make_uint4(k[j], k[j], k[j], k[j]);
+                    p4[0] = v; p4[1] = v; p4[2] = v; p4[3] = v;
+                }
+                continue;
+            }
+            b[pos] = k[j];
         }
     }
 }
@@ -169,6 +218,10 @@ int main() {
         t = timeit([&] { k_copy_tile<<<g, 1024>>>(in, out, ntiles); });
         printf("copy-tile  %.4f ms  %7.1f GB/s  (grid %d)\n", t, gb / t * 1e3, g);
     }
+    t = timeit([&] { k_copy_tile_sh<7><<<256, 1024>>>(in, out, ntiles); });
+    printf("copy-tile+7  %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_copy_tile_sh<16><<<256, 1024>>>(in, out, ntiles); });
+    printf("copy-tile+16 %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { k_read<<<8192, 256>>>((const uint4 *)in, n / 4, sink); });
     printf("read       %.4f ms  %7.1f GB/s\n", t, gb / 2 / t * 1e3);
     t = timeit([&] { k_write<<<8192, 256>>>((uint4 *)out, n / 4); });
@@ -185,6 +238,18 @@ int main() {
     printf("abut-64    %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { k_abut<64, 1, 1><<<256, 1024>>>(in, out, ntiles); });
     printf("abut-64xl  %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut<64, 1, 1, 0, 0, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-64xl-ho %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut<32, 1, 1, 0, 0, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-32xl-ho %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut<64, 1, 0, 0, 0, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-64-ho %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_own<64, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-64xl-own %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_own<64, 0><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-64-own %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_own<32, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-32xl-own %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { k_abut<64, 1, 1, 1><<<256, 1024>>>(in, out, ntiles); });
     printf("abut-64xlnt %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { k_abut<64, 1, 0, 0, 1><<<256, 1024>>>(in, out, ntiles); });
@@ -213,6 +278,12 @@ int main() {
     printf("abut-32    %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { k_abut<16, 1><<<256, 1024>>>(in, out, ntiles); });
     printf("abut-16    %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut<8, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-8     %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut<16, 1, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-16xl  %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut<8, 1, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("abut-8xl   %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
     CK(hipDeviceSynchronize());
     return 0;
 }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# XCD-grouped acquisition experiment: GPU sort tests, then bench + per-pass times for
+# A/B experiment (first used for XCD-grouped acquisition): GPU sort tests ($TESTS), then bench + per-pass times for
 # the library (XCD groups) and harness/exp/liblabsort_stamps_x0.so (one global counter),
 # each with LABSORT_SEG=first (default) and on.
 set -o pipefail
@@ -7,7 +7,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 O="$R/gpurun_out"; mkdir -p "$O"; cd /tmp && export TMPDIR=/tmp
 P=radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd/liblabsort.so
 if [ -z "$NOTEST" ]; then
-  timeout -k 10 300 python -m pytest "$R/tests/test_gpu_sort.py" -x -q -p no:cacheprovider > "$O/xt.log" 2>&1 || { tail -30 "$O/xt.log"; exit 1; }
+  timeout -k 10 300 python -m pytest ${TESTS:-"$R/tests/test_gpu_sort.py"} -x -q -p no:cacheprovider > "$O/xt.log" 2>&1 || { tail -30 "$O/xt.log"; exit 1; }
   tail -2 "$O/xt.log"
 fi
 for lib in $P ${LIBS-harness/exp/liblabsort_stamps_x0.so}; do

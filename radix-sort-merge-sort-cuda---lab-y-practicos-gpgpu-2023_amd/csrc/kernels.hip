@@ -1554,13 +1554,15 @@ hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32
 }
 
 // Look-back chains per pass (LABSORT_SEG, read once per process):
-//   "first" (default): NSEG position segments in the first active pass, one chain in
-//            the later passes (no joint histograms counted);
-//   "on":    also digit-group segments in the later passes (joint histograms);
+//   "on" (default, OSP_SEG_LATER = 1): NSEG position segments in the first active
+//            pass, digit-group segments in the later passes (joint histograms
+//            counted by k_hist_seg);
+//   "first": position segments in the first active pass, one chain in the later
+//            passes;
 //   "none":  one chain in every pass.
-// Measured on MI355X at 2^28 (r09): the later passes run 1-2 % faster as one chain
-// than as digit-group segments plus joint counting, and position segments gain ~1 %
-// in the first pass.
+// Measured on MI355X at 2^28: with XCD-grouped acquisition the digit-group segments
+// gain ~4 % over one chain in the later passes (r13 -> r14); without it (r09) one
+// chain was 1-2 % faster.
 static int seg_later() {
     static int v = 2;
     if (v == 2) {
