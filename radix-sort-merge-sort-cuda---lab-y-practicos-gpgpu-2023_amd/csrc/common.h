@@ -65,7 +65,7 @@ static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass til
 // decoupled look-back chain; a segment's base offsets come from histograms the
 // upfront histogram kernel computes (see k_hist_seg / k_plan8).
 constexpr int NSEG = 16;
-constexpr int HS_BPS = 16;  // histogram workgroups per position segment
+constexpr int HS_BPS = 32;  // histogram workgroups per position segment (2 per CU: 80 KB LDS each)
 // first position of segment s of an n-key pass input (first active pass)
 __host__ __device__ inline uint32_t seg_start(uint32_t s, size_t n) { return (uint32_t)((size_t)s * n / NSEG); }
 struct SegPlan {

@@ -320,14 +320,24 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
         const size_t nv = (end - vbeg) / 4;
         const uint4 *v = reinterpret_cast<const uint4 *>(keys + vbeg);
         size_t i = threadIdx.x;
-        for (; i + 3 * HIST_BLOCK < nv; i += 4 * HIST_BLOCK) {
-            uint4 x[4];
+        // software-pipelined: the next 4 x uint4 load while the current ones are counted
+        // (harness/exp/hist_probe.hip: 0.246 -> 0.204 ms at 2^28)
+        uint4 c[4], x[4];
+        if (i + 3 * HIST_BLOCK < nv) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) x[u] = v[i + u * HIST_BLOCK];
+            for (int u = 0; u < 4; ++u) c[u] = v[i + u * HIST_BLOCK];
+        }
+        for (; i + 3 * HIST_BLOCK < nv; i += 4 * HIST_BLOCK) {
+            if (i + 7 * HIST_BLOCK < nv) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) x[u] = v[i + (4 + u) * HIST_BLOCK];
+            }
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                count(x[u].x); count(x[u].y); count(x[u].z); count(x[u].w);
+                count(c[u].x); count(c[u].y); count(c[u].z); count(c[u].w);
             }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = x[u];
         }
         for (; i < nv; i += HIST_BLOCK) {
             const uint4 x = v[i];
