@@ -49,6 +49,41 @@ __global__ __launch_bounds__(1024) void k_copy_tile_sh(const uint32_t *a, uint32
         for (int j = 0; j < 16; ++j) d[j * 64] = k[j];
     }
 }
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+// copy with U uint4 per thread per step in flight (grid-stride), optionally nontemporal
+template <int U, int NT>
+__global__ __launch_bounds__(256) void k_copy_u(const v4u *a, v4u *b, size_t n4) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+    for (; i + (U - 1) * stride < n4; i += U * stride) {
+        v4u v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(a + i + u * stride) : a[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (NT) __builtin_nontemporal_store(v[u], b + i + u * stride);
+            else b[i + u * stride] = v[u];
+        }
+    }
+    for (; i < n4; i += stride) b[i] = a[i];
+}
+// tiled copy (16384 words per 1024-thread tile) with uint4 per lane: 4 x uint4 per thread
+template <int NT>
+__global__ __launch_bounds__(1024) void k_copy_tile4(const v4u *a, v4u *b, uint32_t ntiles) {
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const v4u *s = a + (size_t)t * 4096 + tid;
+        v4u k[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k[j] = NT ? __builtin_nontemporal_load(s + j * 1024) : s[j * 1024];
+        v4u *d = b + (size_t)t * 4096 + tid;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (NT) __builtin_nontemporal_store(k[j], d + j * 1024);
+            else d[j * 1024] = k[j];
+        }
+    }
+}
 __global__ __launch_bounds__(256) void k_read(const uint4 *a, size_t n4, uint32_t *sink) {
     uint32_t x = 0;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
@@ -217,6 +252,20 @@ int main() {
     for (int g : {256, 512, 1024}) {
         t = timeit([&] { k_copy_tile<<<g, 1024>>>(in, out, ntiles); });
         printf("copy-tile  %.4f ms  %7.1f GB/s  (grid %d)\n", t, gb / t * 1e3, g);
+    }
+    for (int g : {1024, 2048, 4096, 8192}) {
+        t = timeit([&] { k_copy_u<4, 0><<<g, 256>>>((const v4u *)in, (v4u *)out, n / 4); });
+        printf("copy-u4    %.4f ms  %7.1f GB/s  (grid %d)\n", t, gb / t * 1e3, g);
+        t = timeit([&] { k_copy_u<4, 1><<<g, 256>>>((const v4u *)in, (v4u *)out, n / 4); });
+        printf("copy-u4nt  %.4f ms  %7.1f GB/s  (grid %d)\n", t, gb / t * 1e3, g);
+    }
+    t = timeit([&] { k_copy_u<8, 0><<<2048, 256>>>((const v4u *)in, (v4u *)out, n / 4); });
+    printf("copy-u8    %.4f ms  %7.1f GB/s  (grid 2048)\n", t, gb / t * 1e3);
+    for (int g : {256, 512, 1024}) {
+        t = timeit([&] { k_copy_tile4<0><<<g, 1024>>>((const v4u *)in, (v4u *)out, ntiles); });
+        printf("copy-tile4   %.4f ms  %7.1f GB/s  (grid %d)\n", t, gb / t * 1e3, g);
+        t = timeit([&] { k_copy_tile4<1><<<g, 1024>>>((const v4u *)in, (v4u *)out, ntiles); });
+        printf("copy-tile4nt %.4f ms  %7.1f GB/s  (grid %d)\n", t, gb / t * 1e3, g);
     }
     t = timeit([&] { k_copy_tile_sh<7><<<256, 1024>>>(in, out, ntiles); });
     printf("copy-tile+7  %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);

@@ -101,6 +101,16 @@ int labsort_merge_pass(const void *d_in, void *d_out, size_t n, size_t run, int 
  * d_part: >= labsort_merge_parts(d1-d0) words. */
 int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *d_out, size_t d0, size_t d1,
                   int key_type, uint32_t *d_part, void *stream);
+/* K-way merge of up to 8 sorted runs lying back to back in d_in: run q =
+ * d_in[h_offsets[q] .. h_offsets[q+1]), q < nruns (host array of nruns+1 offsets).
+ * Writes the merged keys to d_out[h_offsets[0] .. h_offsets[nruns]) (d_out != d_in);
+ * equal keys keep run order (stable).  One pass over HBM: the multi-GPU exchange
+ * merges the p runs it receives with it, the merge sort's passes use the same
+ * kernels.  Generalises separators_kernel + merge_segments_kernel (lab.cu:209-300)
+ * from 2 to K runs.  d_ws: >= labsort_merge_runs_workspace_bytes(h_offsets[nruns]). */
+size_t labsort_merge_runs_workspace_bytes(size_t n);
+int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, int nruns, int key_type,
+                       void *d_workspace, size_t ws_bytes, void *stream);
 /* d_hist[p * 2^bits + digit] += count of keys with that digit in pass p
  * (p = 0 .. ceil(32/bits)-1); bits = 8 or 1.  d_hist must be zeroed by the caller. */
 int labsort_histogram(const void *d_keys, size_t n, int key_type, int bits, uint32_t *d_hist, void *stream);

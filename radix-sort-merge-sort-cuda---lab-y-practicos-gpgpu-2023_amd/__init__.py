@@ -39,6 +39,7 @@ C_SYMBOLS = [
     "labsort_sort_device", "labsort_sort_host", "labsort_wave_tile_sort", "labsort_tile_sort",
     "labsort_merge_parts", "labsort_merge_pass", "labsort_merge", "labsort_histogram", "labsort_fill",
     "labsort_count_descents", "labsort_timing_enable", "labsort_timing_read", "labsort_upper_bound", "sort",
+    "labsort_merge_runs_workspace_bytes", "labsort_merge_runs",
 ]
 CXX_SYMBOLS = ["_Z11order_arrayPii", "_Z16order_with_trustPii"]
 
@@ -82,6 +83,9 @@ def _load() -> ctypes.CDLL:
     L.labsort_tile_sort.argtypes = [p, p, sz, i, p]
     L.labsort_merge_pass.argtypes = [p, p, sz, sz, i, p, p]
     L.labsort_merge.argtypes = [p, sz, p, sz, p, sz, sz, i, p, p]
+    L.labsort_merge_runs_workspace_bytes.restype = sz
+    L.labsort_merge_runs_workspace_bytes.argtypes = [sz]
+    L.labsort_merge_runs.argtypes = [p, p, ctypes.POINTER(sz), i, i, p, sz, p]
     L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
     L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
     L.labsort_count_descents.argtypes = [p, sz, i, p, p]
@@ -214,6 +218,23 @@ def merge_pass(d_in, d_out, n: int, run: int, d_part, key: str = "u32", stream=N
 def merge(d_a, la: int, d_b, lb: int, d_out, d0: int, d1: int, d_part, key: str = "u32", stream=None) -> None:
     _check(lib.labsort_merge(_ptr(d_a) if la else 0, la, _ptr(d_b) if lb else 0, lb, _ptr(d_out), d0, d1,
                              KEY[key], _ptr(d_part), _stream(stream)), "merge")
+
+
+def merge_runs_workspace_bytes(n: int) -> int:
+    return int(lib.labsort_merge_runs_workspace_bytes(n))
+
+
+def merge_runs(d_in, d_out, offsets, key: str = "u32", workspace=None, stream=None) -> None:
+    """K-way merge (K <= 8) of the sorted runs d_in[offsets[q]:offsets[q+1]] into
+    d_out[offsets[0]:offsets[-1]] (stable: equal keys keep run order)."""
+    offs = [int(x) for x in offsets]
+    if workspace is None:
+        import torch
+        workspace = torch.empty(max(merge_runs_workspace_bytes(offs[-1]), 1), dtype=torch.uint8, device="cuda")
+    wsb = workspace.numel() * workspace.element_size()
+    arr = (ctypes.c_size_t * len(offs))(*offs)
+    _check(lib.labsort_merge_runs(_ptr(d_in), _ptr(d_out), arr, len(offs) - 1, KEY[key], _ptr(workspace), wsb,
+                                  _stream(stream)), "merge_runs")
 
 
 def histogram(d_keys, n: int, d_hist, bits: int = 8, key: str = "u32", stream=None) -> None:

@@ -127,7 +127,7 @@ RadixLayout radix_layout(size_t n, int bits) {
 }
 
 struct MergeLayout {
-    size_t off_tmp, off_part, total;
+    size_t off_tmp, off_part, off_km, total;
 };
 MergeLayout merge_layout(size_t n) {
     MergeLayout L{};
@@ -136,6 +136,8 @@ MergeLayout merge_layout(size_t n) {
     o = align_up(o + n * 4, 256);
     L.off_part = o;
     o = align_up(o + (labsort_merge_parts(n)) * 4, 256);
+    L.off_km = o;  // K-way merge samples and block cuts
+    o = align_up(o + km_workspace_words(n) * 4, 256);
     L.total = o;
     return L;
 }
@@ -189,10 +191,20 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
     return LABSORT_OK;
 }
 
+// Merge passes after the tile sort (runs of TS_TILE keys).  KM_SORT_K = 2: the
+// pairwise merge-path pass (k_merge_pass_p); 4 or 8: K-way passes (kmerge.hip), K =
+// KM_SORT_K while that many runs remain, then the smallest power of two covering
+// the rest.
+int merge_pass_k(size_t n, size_t run) {
+    if (KM_SORT_K == 2) return 2;
+    const size_t runs = (n + run - 1) / run;
+    int k = 2;
+    while (k < KM_SORT_K && (size_t)k < runs) k <<= 1;
+    return k;
+}
 int merge_passes(size_t n) {
-    size_t runs = (n + TS_TILE - 1) / TS_TILE;
     int m = 0;
-    while (((size_t)1 << m) < runs) ++m;
+    for (size_t run = TS_TILE; run < n; run *= (size_t)merge_pass_k(n, run)) ++m;
     return m;
 }
 
@@ -200,6 +212,7 @@ int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char 
     const MergeLayout L = merge_layout(n);
     uint32_t *tmp = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
     uint32_t *part = reinterpret_cast<uint32_t *>(ws + L.off_part);
+    uint32_t *kmw = reinterpret_cast<uint32_t *>(ws + L.off_km);
     const int m = merge_passes(n);
     uint32_t *cur = (m % 2 == 0) ? out : tmp;
     {
@@ -209,10 +222,21 @@ int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char 
     size_t run = TS_TILE;
     for (int k = 0; k < m; ++k) {
         uint32_t *nxt = (cur == out) ? tmp : out;
+        const int K = merge_pass_k(n, run);
         TimingScope ts(LABSORT_K_MERGE, s);
-        HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s));
+        if (KM_SORT_K == 2) {
+            HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s));
+        } else {
+            KmRuns rs{};
+            rs.explicit_runs = 0;
+            rs.K = (uint32_t)K;
+            rs.n = (uint32_t)n;
+            rs.run = (uint32_t)run;
+            rs.njobs = (uint32_t)((n + rs.K * run - 1) / (rs.K * run));
+            HIP_TRY(launch_kmerge(cur, nxt, rs, flip, kmw, s));
+        }
         cur = nxt;
-        run *= 2;
+        run *= (size_t)K;
     }
     return LABSORT_OK;
 }
@@ -378,6 +402,38 @@ int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *
     TimingScope ts(LABSORT_K_MERGE, as_stream(stream));
     HIP_TRY(launch_merge_ab(static_cast<const uint32_t *>(d_a), la, static_cast<const uint32_t *>(d_b), lb,
                             static_cast<uint32_t *>(d_out), d0, d1, flip_of(key_type), d_part, as_stream(stream)));
+    return LABSORT_OK;
+}
+
+size_t labsort_merge_runs_workspace_bytes(size_t n) { return km_workspace_words(n) * 4; }
+
+int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, int nruns, int key_type,
+                       void *d_ws, size_t ws_bytes, void *stream) {
+    if (nruns < 1 || nruns > 8 || !h_offsets) return LABSORT_ERR_ARG;
+    const size_t n = h_offsets[nruns] - h_offsets[0];
+    for (int q = 0; q < nruns; ++q)
+        if (h_offsets[q + 1] < h_offsets[q]) return LABSORT_ERR_ARG;
+    if (h_offsets[nruns] > 0xFFFFFFFFu || n > 0x7FFFFFFFu) return LABSORT_ERR_ARG;
+    if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
+    if (n == 0) return LABSORT_OK;
+    if (!d_in || !d_out || d_in == d_out) return LABSORT_ERR_ARG;
+    if (!d_ws || ws_bytes < labsort_merge_runs_workspace_bytes(h_offsets[nruns])) return LABSORT_ERR_ARG;
+    hipStream_t s = as_stream(stream);
+    if (nruns == 1) {
+        HIP_TRY(hipMemcpyAsync(static_cast<uint32_t *>(d_out) + h_offsets[0],
+                               static_cast<const uint32_t *>(d_in) + h_offsets[0], n * 4, hipMemcpyDeviceToDevice, s));
+        return LABSORT_OK;
+    }
+    KmRuns rs{};
+    rs.explicit_runs = 1;
+    rs.K = 2;
+    while ((int)rs.K < nruns) rs.K <<= 1;
+    for (uint32_t q = 0; q <= rs.K; ++q) rs.offs[q] = (uint32_t)h_offsets[(int)q < nruns ? q : nruns];
+    rs.n = (uint32_t)h_offsets[nruns];
+    rs.njobs = 1;
+    TimingScope ts(LABSORT_K_MERGE, s);
+    HIP_TRY(launch_kmerge(static_cast<const uint32_t *>(d_in), static_cast<uint32_t *>(d_out), rs, flip_of(key_type),
+                          static_cast<uint32_t *>(d_ws), s));
     return LABSORT_OK;
 }
 

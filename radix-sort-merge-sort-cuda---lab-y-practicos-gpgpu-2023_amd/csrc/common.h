@@ -102,6 +102,41 @@ constexpr int MG_MAX_TPB = 256;       // most consecutive output tiles per merge
 constexpr int MG_BRACKET = LABSORT_MG_BRACKET;  // co-rank search: every 8th tile first, the rest bracketed
 constexpr int MG_BLOCKS_PER_CU = 8;  // persistent merge pass grid  // 4096 outputs per workgroup
 
+// ---- K-way merge (kmerge.hip) ----
+// (overridable for diagnostic builds under harness/exp)
+#ifndef LABSORT_KM_S
+#define LABSORT_KM_S 256
+#endif
+#ifndef LABSORT_KM_M
+#define LABSORT_KM_M 16
+#endif
+#ifndef LABSORT_KM_BLOCK
+#define LABSORT_KM_BLOCK 512
+#endif
+#ifndef LABSORT_KM_SEQ
+#define LABSORT_KM_SEQ 0
+#endif
+constexpr uint32_t KM_S = LABSORT_KM_S;  // sample stride (the reference's separators: every 256 keys)
+constexpr uint32_t KM_M = LABSORT_KM_M;  // samples per block: blocks average KM_M * KM_S keys
+constexpr int KM_BLOCK = LABSORT_KM_BLOCK;  // threads per block-merge workgroup
+constexpr bool KM_SEQ = LABSORT_KM_SEQ != 0;  // per-thread chunk: sequential merge (1) or bitonic (0)
+#ifndef LABSORT_KM_SORT_K
+#define LABSORT_KM_SORT_K 2
+#endif
+constexpr int KM_SORT_K = LABSORT_KM_SORT_K;  // merge sort: 2 = pairwise merge-path passes, 4/8 = K-way passes
+#define KM_BMAX(K) ((KM_M + (K)) * KM_S)  // most keys in one block
+struct KmRuns {
+    uint32_t explicit_runs;  // 1: one job, runs [offs[q], offs[q+1]); 0: runs of `run` keys tiling [0, n)
+    uint32_t K;              // runs per job: 2, 4 or 8 (missing runs are empty)
+    uint32_t n;
+    uint32_t run;            // uniform: run length (a multiple of KM_S)
+    uint32_t njobs;          // uniform: ceil(n / (K * run)); explicit: 1
+    uint32_t nspl_max;       // set by launch_kmerge: splitters of the largest job
+    uint32_t offs[9];
+};
+hipError_t launch_kmerge(const uint32_t *in, uint32_t *out, KmRuns rs, uint32_t flip, uint32_t *ws, hipStream_t s);
+size_t km_workspace_words(size_t n);
+
 constexpr int MAX_PASSES = 32;
 constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_SKIP = 0xFFu;
 constexpr uint32_t NEXT_NONE = 0xFFFFFFFFu;

@@ -20,8 +20,8 @@ sorts its shard, the ranks agree on p-1 splitters from a regular sample of every
 shard (one all_gather), cut their sorted shards at the splitters
 (`labsort_upper_bound`), send piece j to rank j with pairwise send/recv posted to
 all peers at once (so all 7 xGMI links of a node carry data together instead of
-one per step), and merge the p received runs in rank order with a merge tree
-(`labsort_merge`, A before B on ties).  Rank r then holds the r-th contiguous
+one per step) straight into one buffer, and merge the p received runs in rank
+order in one K-way pass (`labsort_merge_runs`, A before B on ties).  Rank r then holds the r-th contiguous
 range of the sorted array; range sizes follow the splitters (within a few percent
 of n/p on varied data; skewed data with a heavy repeated key can unbalance them).
 
@@ -49,6 +49,25 @@ class Ops:
     def merge(self, a: torch.Tensor, b: torch.Tensor, d0: int, d1: int) -> torch.Tensor:
         """elements d0..d1-1 of merge(a, b), a before b on ties"""
         raise NotImplementedError
+
+    def merge_runs(self, buf: torch.Tensor, offsets: list) -> torch.Tensor:
+        """Merge of the sorted runs buf[offsets[q]:offsets[q+1]] in run order (equal
+        keys keep run order).  Default: a tree of pairwise merges."""
+        runs = [buf[offsets[q]:offsets[q + 1]] for q in range(len(offsets) - 1)]
+        while len(runs) > 1:
+            nxt = []
+            for i in range(0, len(runs) - 1, 2):
+                x, y = runs[i], runs[i + 1]
+                if x.numel() == 0:
+                    nxt.append(y)
+                elif y.numel() == 0:
+                    nxt.append(x)
+                else:
+                    nxt.append(self.merge(x, y, 0, x.numel() + y.numel()))
+            if len(runs) % 2:
+                nxt.append(runs[-1])
+            runs = nxt
+        return runs[0].contiguous() if runs else buf[:0]
 
     def key_le(self, x: int, y: int) -> bool:
         raise NotImplementedError
@@ -90,6 +109,24 @@ class HipOps(Ops):
             self._part = torch.empty(parts, dtype=torch.int32, device=out.device)
         self.ls.merge(a, a.numel(), b, b.numel(), out, d0, d1, self._part, key=self.key, stream=self.stream)
         return out[: d1 - d0]
+
+    def merge_runs(self, buf, offsets):
+        """One K-way pass (labsort_merge_runs, K <= 8); more runs: the merge tree."""
+        if len(offsets) - 1 > 8:
+            return super().merge_runs(buf, offsets)
+        n = offsets[-1] - offsets[0]
+        out = torch.empty(max(n, 1), dtype=torch.int32, device=buf.device)
+        if n:
+            o = [x - offsets[0] for x in offsets]
+            self.ls.merge_runs(buf[offsets[0]:offsets[-1]], out, o, key=self.key, workspace=self._kmws(n),
+                               stream=self.stream)
+        return out[:n]
+
+    def _kmws(self, n):
+        need = max(self.ls.merge_runs_workspace_bytes(n), 256)
+        if getattr(self, "_km", None) is None or self._km.numel() < need:
+            self._km = torch.empty(need, dtype=torch.uint8, device="cuda")
+        return self._km
 
     def key_le(self, x, y):
         f = 0x80000000 if self.key == "i32" else 0
@@ -280,22 +317,15 @@ def dist_sort_splitters(local: torch.Tensor, ops: Ops, group=None, comm=None, co
     sizes = torch.tensor([bounds[j + 1] - bounds[j] for j in range(world)], dtype=torch.int64, device=a.device)
     all_sizes = torch.stack(comm.all_gather(sizes)).cpu()  # all_sizes[i][j] = rank i -> rank j
     sends = [a[bounds[j]:bounds[j + 1]] for j in range(world)]
-    recvs = [torch.empty(int(all_sizes[i][rank]), dtype=a.dtype, device=a.device) if i != rank else sends[rank]
-             for i in range(world)]
+    # receive every piece straight into its slot of one buffer (rank order), then one
+    # K-way merge pass over the p runs (A before B on ties, so equal keys keep rank order)
+    counts = [int(all_sizes[i][rank]) for i in range(world)]
+    offs = [0]
+    for c in counts:
+        offs.append(offs[-1] + c)
+    buf = torch.empty(max(offs[-1], 1), dtype=a.dtype, device=a.device)
+    recvs = [buf[offs[i]:offs[i + 1]] for i in range(world)]
+    if counts[rank]:
+        recvs[rank].copy_(sends[rank])
     comm.exchange_all([x.contiguous() for x in sends], recvs, rank)
-    # merge the p sorted runs in rank order (merge tree, A before B on ties)
-    runs = [r for r in recvs]
-    while len(runs) > 1:
-        nxt = []
-        for i in range(0, len(runs) - 1, 2):
-            x, y = runs[i], runs[i + 1]
-            if x.numel() == 0:
-                nxt.append(y)
-            elif y.numel() == 0:
-                nxt.append(x)
-            else:
-                nxt.append(ops.merge(x, y, 0, x.numel() + y.numel()))
-        if len(runs) % 2:
-            nxt.append(runs[-1])
-        runs = nxt
-    return runs[0].contiguous()
+    return ops.merge_runs(buf, offs)

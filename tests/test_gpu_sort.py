@@ -182,6 +182,48 @@ def test_merge_diagonal_ranges(ls, oracle, torch_gpu, la, lb):
         np.testing.assert_array_equal(from_dev(out), oracle.merge_split(A, B, d0, d1))
 
 
+@pytest.mark.parametrize("lens", [
+    [5000, 7000],                                  # K = 2
+    [1, 0, 3, 2],                                  # tiny and empty runs, K = 4
+    [100_000, 99_999, 1, 0, 65_536, 70_001, 512, 4096],  # K = 8, ragged
+    [300_000, 0, 0, 0, 0],                         # one non-empty run of five (K = 8)
+    [40_000] * 3,                                  # three equal runs (K = 4, one empty)
+    [1 << 18] * 8,                                 # eight equal runs
+])
+@pytest.mark.parametrize("dist,key", [("mod1000", "u32"), ("u32", "i32"), ("const", "u32"), ("u32", "u32")])
+def test_merge_runs(ls, oracle, torch_gpu, lens, dist, key):
+    """K-way merge of the runs one rank receives in the multi-GPU exchange (and of the
+    merge sort's passes): equals std::sort of the concatenation, base offset > 0."""
+    torch = torch_gpu
+    base = 37
+    n = sum(lens)
+    a = oracle.gen(n, SEED + 20 + len(lens), dist)
+    offs, pos, runs = [base], base, []
+    for q, L in enumerate(lens):
+        runs.append(ref_sort(oracle, a[pos - base:pos - base + L], key))
+        pos += L
+        offs.append(pos)
+    buf = np.concatenate([np.zeros(base, np.uint32)] + runs + [np.zeros(5, np.uint32)])
+    t = to_dev(torch, buf)
+    o = torch.full_like(t, 12345)
+    ls.merge_runs(t, o, offs, key=key)
+    torch.cuda.synchronize()
+    got = from_dev(o)
+    np.testing.assert_array_equal(got[base:base + n], ref_sort(oracle, a, key))
+    assert (got[:base] == 12345).all() and (got[base + n:] == 12345).all()
+
+
+def test_merge_runs_bad_args(ls, torch_gpu):
+    torch = torch_gpu
+    t = torch.zeros(16, dtype=torch.int32, device="cuda")
+    with pytest.raises(ls.LabsortError):
+        ls.merge_runs(t, t, [0, 8, 16])            # in place
+    with pytest.raises(ls.LabsortError):
+        ls.merge_runs(t, torch.zeros_like(t), [0, 9, 8])  # decreasing offsets
+    with pytest.raises(ls.LabsortError):
+        ls.merge_runs(t, torch.zeros_like(t), list(range(11)))  # 10 runs > 8
+
+
 # ---- host-pointer drop-ins (lab.h) ------------------------------------------------------------
 @pytest.mark.parametrize("n", [256, 1024, 65536, 1 << 17, 1 << 20])
 def test_order_array_matches_std_sort(ls, oracle, torch_gpu, n):
