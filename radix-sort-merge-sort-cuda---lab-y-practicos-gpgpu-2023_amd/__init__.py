@@ -27,7 +27,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LABSORT_LIBRARY") or os.path.join(HERE, "liblabsort.so")
 
 OK, ERR_ARG, ERR_HIP, ERR_DEVICE = 0, 1, 2, 3
-ALGO = {"radix": 0, "merge": 1, "radix1": 2}
+ALGO = {"radix": 0, "merge": 1, "radix1": 2, "auto": 3}
 KEY = {"u32": 0, "i32": 1}
 DIST = {"u32": 0, "u31": 1, "mod100": 2, "mod1000": 3, "sorted": 4, "reversed": 5, "const": 6, "lowbits": 7}
 KCLASS = {"histogram": 0, "onesweep": 1, "tile_sort": 2, "merge": 3, "partition": 4}
@@ -166,7 +166,9 @@ def order_with_trust(a: np.ndarray) -> None:
 
 
 def _default_algo() -> int:
-    return ALGO.get(os.environ.get("LABSORT_ALGO", "radix"), 0)
+    """as the C++ drop-ins: LABSORT_ALGO names the algorithm, else "auto" (merge up to
+    LABSORT_AUTO_MERGE_MAX_KEYS keys, radix above)"""
+    return ALGO.get(os.environ.get("LABSORT_ALGO", "auto"), ALGO["auto"])
 
 
 # ---- device API (torch tensors or raw device addresses) ----------------------------

@@ -269,10 +269,19 @@ int ensure_buffer(void **p, size_t *have, size_t need) {
 
 int default_algo() {
     const char *e = std::getenv("LABSORT_ALGO");
-    if (!e) return LABSORT_ALGO_RADIX;
+    if (!e) return LABSORT_ALGO_AUTO;
     if (!std::strcmp(e, "merge")) return LABSORT_ALGO_MERGE;
     if (!std::strcmp(e, "radix1")) return LABSORT_ALGO_RADIX1;
-    return LABSORT_ALGO_RADIX;
+    if (!std::strcmp(e, "radix")) return LABSORT_ALGO_RADIX;
+    return LABSORT_ALGO_AUTO;
+}
+
+// LABSORT_ALGO_AUTO -> the algorithm that runs.  Measured on MI355X (r15,
+// harness/exp/small_n.py, device-resident): merge 0.054 / 0.119 / 0.202 ms vs radix
+// 0.134 / 0.220 / 0.286 ms at 2^16 / 2^20 / 2^22; equal at 2^23; radix faster above.
+int resolve_algo(int algo, size_t n) {
+    if (algo != LABSORT_ALGO_AUTO) return algo;
+    return n <= (size_t)LABSORT_AUTO_MERGE_MAX_KEYS ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
 }
 
 }  // namespace
@@ -306,6 +315,7 @@ size_t labsort_merge_tile_keys(void) { return (size_t)MG_TILE; }
 size_t labsort_merge_parts(size_t n) { return (n + MG_TILE - 1) / MG_TILE + 2; }
 
 size_t labsort_workspace_bytes(size_t n, int algo) {
+    algo = resolve_algo(algo, n);
     if (small_path(n, algo)) return 256;
     switch (algo) {
     case LABSORT_ALGO_RADIX: return radix_layout(n, 8).total;
@@ -320,9 +330,11 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
     if (n == 0) return LABSORT_OK;
     if (!d_in || !d_out) return LABSORT_ERR_ARG;
     if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
-    if (algo != LABSORT_ALGO_RADIX && algo != LABSORT_ALGO_MERGE && algo != LABSORT_ALGO_RADIX1)
+    if (algo != LABSORT_ALGO_RADIX && algo != LABSORT_ALGO_MERGE && algo != LABSORT_ALGO_RADIX1 &&
+        algo != LABSORT_ALGO_AUTO)
         return LABSORT_ERR_ARG;
     if (n > labsort_max_keys(algo)) return LABSORT_ERR_ARG;
+    algo = resolve_algo(algo, n);
     if (ws_bytes < labsort_workspace_bytes(n, algo) || !d_ws) return LABSORT_ERR_ARG;
     const uint32_t flip = flip_of(key_type);
     hipStream_t s = as_stream(stream);
@@ -342,6 +354,7 @@ int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo) {
     if (n == 0) return LABSORT_OK;
     if (!h_keys) return LABSORT_ERR_ARG;
     if (n > labsort_max_keys(algo)) return LABSORT_ERR_ARG;
+    algo = resolve_algo(algo, n);
     std::lock_guard<std::mutex> lk(g_host_mu);
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));

@@ -66,6 +66,7 @@ static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass til
 // upfront histogram kernel computes (see k_hist_seg / k_plan8).
 constexpr int NSEG = 16;
 constexpr int HS_BPS = 32;  // histogram workgroups per position segment (2 per CU: 80 KB LDS each)
+constexpr size_t HS_MIN_KEYS = 65536;  // fewest keys per histogram workgroup below 2^25 keys
 // first position of segment s of an n-key pass input (first active pass)
 __host__ __device__ inline uint32_t seg_start(uint32_t s, size_t n) { return (uint32_t)((size_t)s * n / NSEG); }
 struct SegPlan {
@@ -120,6 +121,14 @@ constexpr uint32_t KM_S = LABSORT_KM_S;  // sample stride (the reference's separ
 constexpr uint32_t KM_M = LABSORT_KM_M;  // samples per block: blocks average KM_M * KM_S keys
 constexpr int KM_BLOCK = LABSORT_KM_BLOCK;  // threads per block-merge workgroup
 constexpr bool KM_SEQ = LABSORT_KM_SEQ != 0;  // per-thread chunk: sequential merge (1) or bitonic (0)
+#ifndef LABSORT_KM_PERSIST
+#define LABSORT_KM_PERSIST 0
+#endif
+#ifndef LABSORT_KM_PERSIST_OVER
+#define LABSORT_KM_PERSIST_OVER 1
+#endif
+constexpr bool KM_PERSIST = LABSORT_KM_PERSIST != 0;  // persistent pipelined block merge (k_km_blocks_p)
+constexpr int KM_PERSIST_OVER = LABSORT_KM_PERSIST_OVER;  // persistent grid = CUs x fit x this
 #ifndef LABSORT_KM_SORT_K
 #define LABSORT_KM_SORT_K 2
 #endif

@@ -292,7 +292,8 @@ __global__ __launch_bounds__(256) void k_plan(const uint32_t *__restrict__ hist,
 //     (A pass whose previous active digit is not p - 1 runs as one chain.)
 // ---------------------------------------------------------------------------------
 __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restrict__ keys, size_t n, uint32_t flip,
-                                                         uint32_t *__restrict__ hps, uint32_t *__restrict__ joint) {
+                                                         uint32_t *__restrict__ hps, uint32_t *__restrict__ joint,
+                                                         uint32_t bps) {
     constexpr int SL = 32;  // replicated digit-0 counters: the 32 lanes of a ds_add group hit 32 banks
     constexpr int JF = 4096;  // 12-bit joint fields per pass
     __shared__ uint32_t h[256 * SL];
@@ -307,9 +308,9 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
 #pragma unroll
         for (int p = 0; p < 3; ++p) atomicAdd(&hj[p * JF + ((k >> (8 * p + 4)) & (JF - 1))], 1u);
     };
-    const uint32_t seg = blockIdx.x / HS_BPS, part = blockIdx.x % HS_BPS;
+    const uint32_t seg = blockIdx.x / bps, part = blockIdx.x % bps;
     const size_t sb = seg_start(seg, n), se = seg_start(seg + 1, n);
-    const size_t per = (se - sb + HS_BPS - 1) / HS_BPS;
+    const size_t per = (se - sb + bps - 1) / bps;
     const size_t beg = sb + (size_t)part * per < se ? sb + (size_t)part * per : se;
     const size_t end = beg + per < se ? beg + per : se;
     if ((((uintptr_t)keys) & 15u) == 0) {
@@ -1559,7 +1560,12 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
 hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, uint32_t *joint,
                            hipStream_t s) {
     if (n == 0) return hipSuccess;
-    k_hist_seg<<<NSEG * HS_BPS, HIST_BLOCK, 0, s>>>(keys, n, flip, hps, joint);
+    // workgroups per position segment: HS_BPS at large n; at small n at least
+    // HS_MIN_KEYS keys each, since every workgroup flushes ~13 K counters with global
+    // atomics (512 workgroups at 2^20: 97 us, contended on the same 48 KB)
+    size_t bps = n / ((size_t)NSEG * HS_MIN_KEYS);
+    bps = bps < 1 ? 1 : bps > (size_t)HS_BPS ? (size_t)HS_BPS : bps;
+    k_hist_seg<<<NSEG * (unsigned)bps, HIST_BLOCK, 0, s>>>(keys, n, flip, hps, joint, (uint32_t)bps);
     return hipGetLastError();
 }
 

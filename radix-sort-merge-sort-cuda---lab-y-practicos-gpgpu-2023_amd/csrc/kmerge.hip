@@ -270,6 +270,176 @@ __global__ __launch_bounds__(KM_BLOCK) void k_km_blocks(const uint32_t *__restri
     for (uint32_t i = tid; i < B; i += KM_BLOCK) out[obase + i] = buf[cur][km_pad(i)];
 }
 
+// Persistent, software-pipelined form of k_km_blocks: workgroup g merges blocks g,
+// g + G, g + 2G, ...  While block i merges in LDS, the keys of block i + G are
+// already loading into registers and the slice header (K cuts) of block i + 2G is
+// in flight, so HBM latency overlaps the LDS merge instead of idling the CU.
+template <int K>
+__device__ __forceinline__ void km_hdr(const KmRuns &rs, const uint32_t *__restrict__ cuts, uint32_t blk, uint32_t q,
+                                       uint32_t &src, uint32_t &len) {
+    const uint32_t bpj = rs.nspl_max + 1u;
+    const uint32_t job = blk / bpj, b = blk % bpj;
+    uint32_t ts = 0;  // samples of this job -> ceil(ts / KM_M) splitters
+#pragma unroll
+    for (int r = 0; r < K; ++r) ts += km_ns(km_re(rs, job, r) - km_rb(rs, job, r));
+    const uint32_t nspl = (ts + KM_M - 1) / KM_M;
+    const uint32_t rb = km_rb(rs, job, q), rl = km_re(rs, job, q) - rb;
+    const uint32_t lo = b == 0 ? 0u : b > nspl ? rl : cuts[((size_t)job * rs.nspl_max + b - 1) * K + q];
+    const uint32_t hi = b >= nspl ? rl : cuts[((size_t)job * rs.nspl_max + b) * K + q];
+    src = rb + lo;
+    len = hi > lo ? hi - lo : 0u;
+}
+
+template <int K>
+struct KmGeo {
+    uint32_t pk[K + 1], sh[K], obase;
+};
+template <int K>
+__device__ __forceinline__ void km_geo(const KmRuns &rs, uint32_t blk, const uint32_t *hs, const uint32_t *hl,
+                                       KmGeo<K> &g) {
+    const uint32_t job = blk / (rs.nspl_max + 1u);
+    g.obase = km_rb(rs, job, 0);
+    g.pk[0] = 0;
+#pragma unroll
+    for (int q = 0; q < K; ++q) {
+        const uint32_t sq = hs[q];
+        g.pk[q + 1] = g.pk[q] + hl[q];
+        g.sh[q] = sq - g.pk[q];
+        g.obase += sq - km_rb(rs, job, q);
+    }
+}
+
+template <int K, int LPT>
+__device__ __forceinline__ void km_load(const uint32_t *__restrict__ in, const KmGeo<K> &g, uint32_t tid,
+                                        uint32_t (&v)[LPT]) {
+    const uint32_t B = g.pk[K];
+#pragma unroll
+    for (int j = 0; j < LPT; ++j) {
+        const uint32_t i = tid + (uint32_t)j * KM_BLOCK;
+        uint32_t s0 = g.sh[0];
+#pragma unroll
+        for (int r = 1; r < K; ++r) s0 = i >= g.pk[r] ? g.sh[r] : s0;
+        v[j] = i < B ? in[i + s0] : 0u;
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(KM_BLOCK) void k_km_blocks_p(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                        KmRuns rs, const uint32_t *__restrict__ cuts, uint32_t flip,
+                                                        uint32_t nblk) {
+    constexpr int LPT = (KM_BMAX(K) + KM_BLOCK - 1) / KM_BLOCK;
+    __shared__ uint32_t buf[2][KM_BMAX(K) + KM_BMAX(K) / 32];
+    __shared__ uint32_t s_hs[2][K], s_hl[2][K];  // slice headers of the next two blocks
+    const uint32_t tid = threadIdx.x, G = gridDim.x;
+    uint32_t blk = blockIdx.x;
+    if (blk >= nblk) return;
+    if (tid < (uint32_t)K) {
+        uint32_t a, l;
+        km_hdr<K>(rs, cuts, blk, tid, a, l);
+        s_hs[0][tid] = a;
+        s_hl[0][tid] = l;
+        if (blk + G < nblk) {
+            km_hdr<K>(rs, cuts, blk + G, tid, a, l);
+            s_hs[1][tid] = a;
+            s_hl[1][tid] = l;
+        }
+    }
+    __syncthreads();
+    KmGeo<K> g;
+    km_geo<K>(rs, blk, s_hs[0], s_hl[0], g);
+    uint32_t v[LPT];
+    km_load<K, LPT>(in, g, tid, v);
+    int slot = 0;  // header slot of blk; blk + G's is slot ^ 1
+    for (;;) {
+        const uint32_t B = g.pk[K];
+#pragma unroll
+        for (int j = 0; j < LPT; ++j) {
+            const uint32_t i = tid + (uint32_t)j * KM_BLOCK;
+            if (i < B) buf[0][km_pad(i)] = v[j];
+        }
+        __syncthreads();  // buf[0] holds blk; s_hs/s_hl[slot ^ 1] hold blk + G
+        const uint32_t nb = blk + G;
+        const bool has_next = nb < nblk;
+        KmGeo<K> gn = g;
+        if (has_next) {
+            km_geo<K>(rs, nb, s_hs[slot ^ 1], s_hl[slot ^ 1], gn);
+            km_load<K, LPT>(in, gn, tid, v);  // in flight during the merge below
+        }
+        uint32_t ha = 0, hl = 0;
+        const bool hh = tid < (uint32_t)K && nb + G < nblk;
+        if (hh) km_hdr<K>(rs, cuts, nb + G, tid, ha, hl);
+        // log2(K) LDS merge levels (as in k_km_blocks)
+        const uint32_t E = ((B + KM_BLOCK - 1) / KM_BLOCK + 7u) & ~7u;
+        int cur = 0;
+#pragma unroll
+        for (int w = 1; w < K; w <<= 1) {
+            const uint32_t *s = buf[cur];
+            uint32_t *d = buf[cur ^ 1];
+            uint32_t pos = tid * E;
+            const uint32_t p1 = pos + E < B ? pos + E : B;
+            while (pos < p1) {
+                uint32_t xs = 0, xm = g.pk[w], ye = g.pk[2 * w];
+#pragma unroll
+                for (int r = 1; r < K / (2 * w); ++r)
+                    if (pos >= g.pk[r * 2 * w]) {
+                        xs = g.pk[r * 2 * w];
+                        xm = g.pk[r * 2 * w + w];
+                        ye = g.pk[(r + 1) * 2 * w];
+                    }
+                const uint32_t lx = xm - xs, ly = ye - xm;
+                const uint32_t end = p1 < ye ? p1 : ye;
+                for (; pos < end; pos += 8) {
+                    const uint32_t diag = pos - xs, cnt = end - pos < 8 ? end - pos : 8;
+                    uint32_t lo = diag > ly ? diag - ly : 0u, hi = diag < lx ? diag : lx;
+                    while (lo < hi) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (km_le(s[km_pad(xs + mid)], s[km_pad(xm + diag - mid - 1)], flip)) lo = mid + 1;
+                        else hi = mid;
+                    }
+                    const uint32_t i = lo, jj = diag - lo;
+                    uint32_t r8[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t xv = i + k < lx ? s[km_pad(xs + i + k)] ^ flip : 0xFFFFFFFFu;
+                        const uint32_t yv = jj + 7 - k < ly ? s[km_pad(xm + jj + 7 - k)] ^ flip : 0xFFFFFFFFu;
+                        r8[k] = xv < yv ? xv : yv;
+                    }
+#pragma unroll
+                    for (int dd = 4; dd >= 1; dd >>= 1)
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            if ((k & dd) == 0) {
+                                const uint32_t a = r8[k], b2 = r8[k + dd];
+                                r8[k] = a < b2 ? a : b2;
+                                r8[k + dd] = a < b2 ? b2 : a;
+                            }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        if ((uint32_t)k < cnt) d[km_pad(pos + k)] = r8[k] ^ flip;
+                }
+                pos = end;
+            }
+            __syncthreads();
+            cur ^= 1;
+        }
+        if (hh) {  // blk's header slot is free: its geometry is in registers
+            s_hs[slot][tid] = ha;
+            s_hl[slot][tid] = hl;
+        }
+        {
+            uint32_t *__restrict__ o = out + g.obase;
+            const uint32_t *f = buf[cur];
+#pragma unroll 4
+            for (uint32_t i = tid; i < B; i += KM_BLOCK) o[i] = f[km_pad(i)];
+        }
+        if (!has_next) break;
+        __syncthreads();  // the output reads are done before buf[0] is refilled
+        g = gn;
+        blk = nb;
+        slot ^= 1;
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
@@ -316,6 +486,32 @@ hipError_t launch_kmerge(const uint32_t *in, uint32_t *out, KmRuns rs, uint32_t 
     }
     const size_t grid = (size_t)rs.njobs * (rs.nspl_max + 1);
     if (grid == 0) return hipGetLastError();
+    if (KM_PERSIST) {
+        // persistent grid: as many workgroups as fit on the chip (LDS-bound), at most one per block
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        }
+        static int fit[9] = {0};
+        if (!fit[rs.K]) {
+            hipError_t e = hipSuccess;
+            switch (rs.K) {
+            case 2: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit[2], k_km_blocks_p<2>, KM_BLOCK, 0); break;
+            case 4: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit[4], k_km_blocks_p<4>, KM_BLOCK, 0); break;
+            default: e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&fit[8], k_km_blocks_p<8>, KM_BLOCK, 0); break;
+            }
+            if (e != hipSuccess || fit[rs.K] <= 0) fit[rs.K] = 1;
+        }
+        size_t g = (size_t)cus * (size_t)fit[rs.K] * (size_t)KM_PERSIST_OVER;
+        if (g > grid) g = grid;
+        switch (rs.K) {
+        case 2: k_km_blocks_p<2><<<(unsigned)g, KM_BLOCK, 0, s>>>(in, out, rs, cuts, flip, (uint32_t)grid); break;
+        case 4: k_km_blocks_p<4><<<(unsigned)g, KM_BLOCK, 0, s>>>(in, out, rs, cuts, flip, (uint32_t)grid); break;
+        default: k_km_blocks_p<8><<<(unsigned)g, KM_BLOCK, 0, s>>>(in, out, rs, cuts, flip, (uint32_t)grid); break;
+        }
+        return hipGetLastError();
+    }
     switch (rs.K) {
     case 2: k_km_blocks<2><<<(unsigned)grid, KM_BLOCK, 0, s>>>(in, out, rs, cuts, flip); break;
     case 4: k_km_blocks<4><<<(unsigned)grid, KM_BLOCK, 0, s>>>(in, out, rs, cuts, flip); break;

@@ -21,7 +21,8 @@ shard (one all_gather), cut their sorted shards at the splitters
 (`labsort_upper_bound`), send piece j to rank j with pairwise send/recv posted to
 all peers at once (so all 7 xGMI links of a node carry data together instead of
 one per step) straight into one buffer, and merge the p received runs in rank
-order in one K-way pass (`labsort_merge_runs`, A before B on ties).  Rank r then holds the r-th contiguous
+order (a tree of `labsort_merge` passes, or one K-way `labsort_merge_runs` pass;
+A before B on ties).  Rank r then holds the r-th contiguous
 range of the sorted array; range sizes follow the splitters (within a few percent
 of n/p on varied data; skewed data with a heavy repeated key can unbalance them).
 
@@ -85,8 +86,13 @@ class Ops:
 class HipOps(Ops):
     """liblabsort.so on the current GPU."""
 
-    def __init__(self, ls, key: str = "u32", local_algo: str = "radix", stream=None):
+    def __init__(self, ls, key: str = "u32", local_algo: str = "radix", stream=None, kway: bool = False):
         self.ls, self.key, self.algo, self.stream = ls, key, local_algo, stream
+        # kway: merge the received runs in one K-way pass (labsort_merge_runs) instead of
+        # the tree of pairwise merge-path passes.  Off by default: on MI355X the tree is
+        # faster (one pairwise pass 0.51 ms vs an 8-way pass ~1.9 ms at 2^28, r15;
+        # the K-way block merge is bound by LDS operations, DESIGN.md section 3.2)
+        self.kway = kway
         self._ws = None
         self._part = None
 
@@ -111,8 +117,9 @@ class HipOps(Ops):
         return out[: d1 - d0]
 
     def merge_runs(self, buf, offsets):
-        """One K-way pass (labsort_merge_runs, K <= 8); more runs: the merge tree."""
-        if len(offsets) - 1 > 8:
+        """One K-way pass (labsort_merge_runs, K <= 8) when self.kway; otherwise (and for
+        more than 8 runs) the merge tree."""
+        if not self.kway or len(offsets) - 1 > 8:
             return super().merge_runs(buf, offsets)
         n = offsets[-1] - offsets[0]
         out = torch.empty(max(n, 1), dtype=torch.int32, device=buf.device)
@@ -317,8 +324,8 @@ def dist_sort_splitters(local: torch.Tensor, ops: Ops, group=None, comm=None, co
     sizes = torch.tensor([bounds[j + 1] - bounds[j] for j in range(world)], dtype=torch.int64, device=a.device)
     all_sizes = torch.stack(comm.all_gather(sizes)).cpu()  # all_sizes[i][j] = rank i -> rank j
     sends = [a[bounds[j]:bounds[j + 1]] for j in range(world)]
-    # receive every piece straight into its slot of one buffer (rank order), then one
-    # K-way merge pass over the p runs (A before B on ties, so equal keys keep rank order)
+    # receive every piece straight into its slot of one buffer (rank order), then merge
+    # the p runs (A before B on ties, so equal keys keep rank order)
     counts = [int(all_sizes[i][rank]) for i in range(world)]
     offs = [0]
     for c in counts:

@@ -84,6 +84,12 @@ def test_sizes_and_limits(ls):
             prev = w
             if n > TS:
                 assert w >= 4 * n  # one ping-pong buffer of n keys
+    # auto (the drop-ins' default): merge up to 2^22 keys, radix above
+    assert ls.max_keys("auto") == ls.max_keys("radix")
+    for n in (1, TS + 1, 1 << 20, 1 << 22):
+        assert ls.workspace_bytes(n, "auto") == ls.workspace_bytes(n, "merge")
+    for n in ((1 << 22) + 1, 1 << 28):
+        assert ls.workspace_bytes(n, "auto") == ls.workspace_bytes(n, "radix")
     # radix at 2^28: tmp keys + 4 passes x 32768 tiles x 256 look-back words + hist
     assert ls.workspace_bytes(1 << 28, "radix") < 4 * (1 << 28) + 4 * 32768 * 256 * 4 + (1 << 20)
 

@@ -39,7 +39,7 @@ def _worker(rank, world, port, cfg, q):
         m = cfg["m"]
         t = torch.empty(m, dtype=torch.int32, device="cuda")
         ls.fill(t, m, cfg["seed"], cfg["dist"], first=rank * m)
-        ops = D.HipOps(ls, key=cfg["key"], local_algo=cfg["algo"])
+        ops = D.HipOps(ls, key=cfg["key"], local_algo=cfg["algo"], kway=cfg.get("kway", False))
         if cfg.get("exchange") == "splitters":
             out = D.dist_sort_splitters(t, ops, copy_input=True, comm=D.HostStagedComm())
         else:
@@ -73,6 +73,9 @@ CFGS = [
     dict(m=1 << 20, dist="u32", seed=0x5EED0008, key="u32", algo="radix", exchange="splitters"),
     dict(m=300_001, dist="mod1000", seed=0x5EED0009, key="i32", algo="radix", exchange="splitters"),
     dict(m=70_000, dist="const", seed=0x5EED000A, key="u32", algo="radix", exchange="splitters"),
+    # received runs merged in one K-way pass (labsort_merge_runs)
+    dict(m=1 << 20, dist="u32", seed=0x5EED000B, key="u32", algo="radix", exchange="splitters", kway=True),
+    dict(m=200_003, dist="mod100", seed=0x5EED000C, key="i32", algo="radix", exchange="splitters", kway=True),
 ]
 
 
