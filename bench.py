@@ -47,7 +47,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--algo", default="radix", choices=["radix", "merge", "radix1"])
+    ap.add_argument("--algo", default="radix", choices=["radix", "merge", "radix1", "pairs"],
+                    help="pairs: stable key/value sort (sort_by_key) of (key, uint32 index) pairs")
     ap.add_argument("--log2n", type=int, default=28, help="keys per GPU = 2^log2n")
     ap.add_argument("--dist", default="u32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -159,6 +160,20 @@ def main():
 
         def barrier():
             dist.barrier()
+    elif args.algo == "pairs":
+        src = torch.empty(n, dtype=torch.int32, device=dev)
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        vsrc = torch.arange(n, dtype=torch.int32, device=dev)
+        vout = torch.empty(n, dtype=torch.int32, device=dev)
+        ws = torch.empty(max(ls.pairs_workspace_bytes(n), 256), dtype=torch.uint8, device=dev)
+        ls.fill(src, n, SEED + 3, args.dist, stream=stream)
+
+        def step():
+            ls.sort_pairs_device(src, vsrc, out, vout, n, key=key, workspace=ws, stream=stream)
+            return out
+
+        def barrier():
+            pass
     else:
         src = torch.empty(n, dtype=torch.int32, device=dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
@@ -228,6 +243,14 @@ def main():
         ok = bool(okt.item())
     else:
         ok, desc = verify(torch, ls, src, res, n, key)
+        if ok and args.algo == "pairs":
+            # each payload is its key's input index: the gather reproduces the output keys,
+            # and equal keys keep ascending indices (stable)
+            idx = vout.to(torch.int64)
+            ok = bool((idx >= 0).all()) and bool((idx < n).all()) and torch.equal(src[idx], res)
+            if ok and n > 1:
+                ok = bool(((vout[1:] > vout[:-1]) | (res[1:] != res[:-1])).all())
+            del idx
     if not ok:
         print(f"bench.py: rank {rank}: OUTPUT CHECK FAILED (sort result is not a sorted permutation)",
               file=sys.stderr)
@@ -239,7 +262,7 @@ def main():
 
     if rank == 0:
         avg_ms = k_ms / k_cnt if k_cnt else None
-        per_launch_bytes = 8.0 * n if dom == "onesweep" else 8.0 * n
+        per_launch_bytes = 16.0 * n if args.algo == "pairs" else 8.0 * n  # key (+ payload) read + written
         achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms else None
         traffic, tsrc = pmc_traffic(dom, n)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
@@ -251,7 +274,9 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds)
         wl = {"radix": "LSD radix sort (8-bit digits, onesweep)", "merge": "LDS tile sort + merge-path passes",
-              "radix1": "LSD radix with 1-bit split passes (letra.pdf)"}[args.algo]
+              "radix1": "LSD radix with 1-bit split passes (letra.pdf)",
+              "pairs": "stable key/value sort (uint32 key + uint32 index payload): LDS tile sort + merge-path "
+                       "passes"}[args.algo]
         if world > 1:
             how = ("splitter exchange (pairwise send/recv to all peers at once) + merge tree"
                    if args.exchange == "splitters" else "bitonic pairwise merge-split network")
@@ -268,7 +293,8 @@ def main():
             "config": {"workload": workload, "n_per_gpu": n, "algo": args.algo if world == 1 else "merge",
                        "key": key, "dist": args.dist,
                        "parallelism": "single GPU" if world == 1 else f"{world} ranks, RCCL {args.exchange} exchange"},
-            "verified": "sorted permutation (descents, digit histograms, sums)",
+            "verified": "sorted permutation (descents, digit histograms, sums)" + (
+                "; payloads gather the output keys, stable" if args.algo == "pairs" and world == 1 else ""),
             "roofline": roofline, "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

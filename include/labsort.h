@@ -90,6 +90,19 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
 /* Host pointer in/out, synchronous: the order_array contract (lab.cu:303). */
 int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo);
 
+/* ---- key/value (sort_by_key; no lab.cu counterpart, the reference sorts
+ * keys only) ----
+ * Stable sort of n (key, 4-byte payload) pairs: d_keys_in/d_vals_in -> d_keys_out/
+ * d_vals_out (out-of-place or fully in place: keys_in == keys_out and vals_in ==
+ * vals_out).  Equal keys keep their input order, so sorting (key, index) pairs gives a
+ * stable argsort, from which payloads of any width can be gathered.  The merge path
+ * with payloads: LDS tile sort of labsort_pair_tile_keys() pairs, then merge-path passes.
+ * Asynchronous on `stream`, no allocation; d_ws >= labsort_pairs_workspace_bytes(n). */
+size_t labsort_pair_tile_keys(void);
+size_t labsort_pairs_workspace_bytes(size_t n);
+int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void *d_keys_out, void *d_vals_out,
+                              size_t n, int key_type, void *d_workspace, size_t workspace_bytes, void *stream);
+
 /* ---- building blocks (exposed for tests and the multi-GPU driver) ---- */
 /* Sort every 64-key tile of d_keys in place by 1-bit splits (ballot + mbcnt +
  * ds_permute), stopping early once the tile is sorted: radix_sort_kernel's job. */
@@ -108,9 +121,9 @@ int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *
 /* K-way merge of up to 8 sorted runs lying back to back in d_in: run q =
  * d_in[h_offsets[q] .. h_offsets[q+1]), q < nruns (host array of nruns+1 offsets).
  * Writes the merged keys to d_out[h_offsets[0] .. h_offsets[nruns]) (d_out != d_in);
- * equal keys keep run order (stable).  One pass over HBM: the multi-GPU exchange
- * merges the p runs it receives with it, the merge sort's passes use the same
- * kernels.  Generalises separators_kernel + merge_segments_kernel (lab.cu:209-300)
+ * equal keys keep run order (stable).  One pass over HBM (the multi-GPU exchange can
+ * merge the p runs it receives with it: HipOps(kway=True); on MI355X the tree of
+ * pairwise passes is faster).  Generalises separators_kernel + merge_segments_kernel (lab.cu:209-300)
  * from 2 to K runs.  d_ws: >= labsort_merge_runs_workspace_bytes(h_offsets[nruns]). */
 size_t labsort_merge_runs_workspace_bytes(size_t n);
 int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, int nruns, int key_type,

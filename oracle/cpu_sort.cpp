@@ -22,6 +22,7 @@
 #include <cstring>
 #include <parallel/algorithm>
 #include <omp.h>
+#include <vector>
 
 extern "C" {
 
@@ -79,6 +80,21 @@ void oracle_par_sort_u32(uint32_t *a, uint64_t n, int threads) {
 
 int oracle_is_sorted_u32(const uint32_t *a, uint64_t n) { return std::is_sorted(a, a + n) ? 1 : 0; }
 int oracle_is_sorted_i32(const int32_t *a, uint64_t n) { return std::is_sorted(a, a + n) ? 1 : 0; }
+
+// Key/value oracle (sort_by_key): std::stable_sort of (key, payload) pairs
+// by key in u32 (flip = 0) or i32 (flip = 0x80000000) order; equal keys keep input order.
+void oracle_stable_sort_pairs(uint32_t *keys, uint32_t *vals, uint64_t n, uint32_t flip) {
+    std::vector<uint64_t> idx(n);
+    for (uint64_t i = 0; i < n; ++i) idx[i] = i;
+    std::stable_sort(idx.begin(), idx.end(), [&](uint64_t x, uint64_t y) { return (keys[x] ^ flip) < (keys[y] ^ flip); });
+    std::vector<uint32_t> k(n), v(n);
+    for (uint64_t i = 0; i < n; ++i) {
+        k[i] = keys[idx[i]];
+        v[i] = vals[idx[i]];
+    }
+    std::memcpy(keys, k.data(), n * 4);
+    std::memcpy(vals, v.data(), n * 4);
+}
 
 // Merge-split oracle for the multi-GPU exchange step: the lower (keep_low=1)
 // or upper half of merge(A, B) with A-before-B on ties (lab.cu:163-170 rule).

@@ -52,6 +52,7 @@ def lib() -> ctypes.CDLL:
         L.oracle_par_sort_u32.argtypes = [p, u64, ctypes.c_int]
         L.oracle_is_sorted_u32.argtypes = [p, u64]
         L.oracle_merge_split_u32.argtypes = [p, u64, p, u64, p, u64, u64]
+        L.oracle_stable_sort_pairs.argtypes = [p, p, u64, ctypes.c_uint32]
         L.oracle_time_sort_u32.argtypes = [p, u64, ctypes.c_int, ctypes.c_int, p]
         L.oracle_time_sort_u32.restype = ctypes.c_double
         L.labcu_order_array.argtypes = [p, ctypes.c_int, ctypes.c_int]
@@ -86,6 +87,15 @@ def sort_i32(a: np.ndarray) -> np.ndarray:
     out = np.ascontiguousarray(a, dtype=np.int32).copy()
     lib().oracle_sort_i32(_ptr(out), out.size)
     return out
+
+
+def stable_sort_pairs(keys: np.ndarray, vals: np.ndarray, key: str = "u32"):
+    """(keys, vals) stably sorted by key (std::stable_sort): the sort_by_key spec."""
+    k = np.ascontiguousarray(keys).view(np.uint32).copy()
+    v = np.ascontiguousarray(vals).view(np.uint32).copy()
+    assert k.size == v.size
+    lib().oracle_stable_sort_pairs(_ptr(k), _ptr(v), k.size, 0x80000000 if key == "i32" else 0)
+    return k, v
 
 
 def merge_split(a: np.ndarray, b: np.ndarray, lo: int, hi: int) -> np.ndarray:

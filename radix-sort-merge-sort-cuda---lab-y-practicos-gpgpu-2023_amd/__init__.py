@@ -40,6 +40,7 @@ C_SYMBOLS = [
     "labsort_merge_parts", "labsort_merge_pass", "labsort_merge", "labsort_histogram", "labsort_fill",
     "labsort_count_descents", "labsort_timing_enable", "labsort_timing_read", "labsort_upper_bound", "sort",
     "labsort_merge_runs_workspace_bytes", "labsort_merge_runs",
+    "labsort_pair_tile_keys", "labsort_pairs_workspace_bytes", "labsort_sort_pairs_device",
 ]
 CXX_SYMBOLS = ["_Z11order_arrayPii", "_Z16order_with_trustPii"]
 
@@ -86,6 +87,11 @@ def _load() -> ctypes.CDLL:
     L.labsort_merge_runs_workspace_bytes.restype = sz
     L.labsort_merge_runs_workspace_bytes.argtypes = [sz]
     L.labsort_merge_runs.argtypes = [p, p, ctypes.POINTER(sz), i, i, p, sz, p]
+    L.labsort_pair_tile_keys.restype = sz
+    L.labsort_pair_tile_keys.argtypes = []
+    L.labsort_pairs_workspace_bytes.restype = sz
+    L.labsort_pairs_workspace_bytes.argtypes = [sz]
+    L.labsort_sort_pairs_device.argtypes = [p, p, p, p, sz, i, p, sz, p]
     L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
     L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
     L.labsort_count_descents.argtypes = [p, sz, i, p, p]
@@ -237,6 +243,26 @@ def merge_runs(d_in, d_out, offsets, key: str = "u32", workspace=None, stream=No
     arr = (ctypes.c_size_t * len(offs))(*offs)
     _check(lib.labsort_merge_runs(_ptr(d_in), _ptr(d_out), arr, len(offs) - 1, KEY[key], _ptr(workspace), wsb,
                                   _stream(stream)), "merge_runs")
+
+
+def pairs_workspace_bytes(n: int) -> int:
+    return int(lib.labsort_pairs_workspace_bytes(n))
+
+
+def pair_tile_keys() -> int:
+    return int(lib.labsort_pair_tile_keys())
+
+
+def sort_pairs_device(d_keys_in, d_vals_in, d_keys_out, d_vals_out, n: int, key: str = "u32", workspace=None,
+                      stream=None) -> None:
+    """Stable sort of n (key, 4-byte payload) pairs (sort_by_key); equal keys keep
+    their input order.  Asynchronous on `stream`."""
+    if workspace is None:
+        import torch
+        workspace = torch.empty(max(pairs_workspace_bytes(n), 1), dtype=torch.uint8, device="cuda")
+    wsb = workspace.numel() * workspace.element_size()
+    _check(lib.labsort_sort_pairs_device(_ptr(d_keys_in), _ptr(d_vals_in), _ptr(d_keys_out), _ptr(d_vals_out), n,
+                                         KEY[key], _ptr(workspace), wsb, _stream(stream)), "sort_pairs_device")
 
 
 def histogram(d_keys, n: int, d_hist, bits: int = 8, key: str = "u32", stream=None) -> None:

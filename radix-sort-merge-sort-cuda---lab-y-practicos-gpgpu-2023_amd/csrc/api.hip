@@ -450,6 +450,56 @@ int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, i
     return LABSORT_OK;
 }
 
+size_t labsort_pair_tile_keys(void) { return (size_t)TS_TILE_KV; }
+
+size_t labsort_pairs_workspace_bytes(size_t n) {
+    if (n <= (size_t)TS_TILE_KV) return 256;
+    return align_up(n * 4, 256) * 2;  // ping-pong keys | payloads
+}
+
+int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void *d_keys_out, void *d_vals_out,
+                              size_t n, int key_type, void *d_ws, size_t ws_bytes, void *stream) {
+    if (n == 0) return LABSORT_OK;
+    if (!d_keys_in || !d_vals_in || !d_keys_out || !d_vals_out) return LABSORT_ERR_ARG;
+    if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
+    if (n > 0x7FFFFFFFu) return LABSORT_ERR_ARG;
+    // in place only as a whole: one side aliased and the other not would read
+    // payloads that the key side's passes already overwrote
+    if ((d_keys_in == d_keys_out) != (d_vals_in == d_vals_out)) return LABSORT_ERR_ARG;
+    if (d_keys_out == d_vals_out) return LABSORT_ERR_ARG;
+    if (!d_ws || ws_bytes < labsort_pairs_workspace_bytes(n)) return LABSORT_ERR_ARG;
+    const uint32_t flip = flip_of(key_type);
+    hipStream_t s = as_stream(stream);
+    const uint32_t *ki = static_cast<const uint32_t *>(d_keys_in), *vi = static_cast<const uint32_t *>(d_vals_in);
+    uint32_t *ko = static_cast<uint32_t *>(d_keys_out), *vo = static_cast<uint32_t *>(d_vals_out);
+    if (n <= (size_t)TS_TILE_KV) {
+        TimingScope ts(LABSORT_K_TILE_SORT, s);
+        HIP_TRY(launch_tile_sort_kv(ki, ko, vi, vo, n, flip, s));
+        return LABSORT_OK;
+    }
+    // merge passes over runs of TS_TILE_KV pairs, ping-pong between out and the workspace;
+    // the tile sort writes where the pass count makes the last pass land in out
+    uint32_t *tk = static_cast<uint32_t *>(d_ws);
+    uint32_t *tv = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + align_up(n * 4, 256));
+    int m = 0;
+    for (size_t run = TS_TILE_KV; run < n; run *= 2) ++m;
+    uint32_t *ck = (m % 2 == 0) ? ko : tk, *cv = (m % 2 == 0) ? vo : tv;
+    {
+        TimingScope ts(LABSORT_K_TILE_SORT, s);
+        HIP_TRY(launch_tile_sort_kv(ki, ck, vi, cv, n, flip, s));
+    }
+    size_t run = TS_TILE_KV;
+    for (int k = 0; k < m; ++k) {
+        uint32_t *nk = (ck == ko) ? tk : ko, *nv = (cv == vo) ? tv : vo;
+        TimingScope ts(LABSORT_K_MERGE, s);
+        HIP_TRY(launch_merge_pass(ck, nk, n, run, flip, nullptr, s, cv, nv));
+        ck = nk;
+        cv = nv;
+        run *= 2;
+    }
+    return LABSORT_OK;
+}
+
 int labsort_histogram(const void *d_keys, size_t n, int key_type, int bits, uint32_t *d_hist, void *stream) {
     if (n == 0) return LABSORT_OK;
     if (!d_keys || !d_hist || (bits != 8 && bits != 1)) return LABSORT_ERR_ARG;

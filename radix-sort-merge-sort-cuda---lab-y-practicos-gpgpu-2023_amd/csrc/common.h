@@ -67,6 +67,10 @@ static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass til
 constexpr int NSEG = 16;
 constexpr int HS_BPS = 32;  // histogram workgroups per position segment (2 per CU: 80 KB LDS each)
 constexpr size_t HS_MIN_KEYS = 65536;  // fewest keys per histogram workgroup below 2^25 keys
+#ifndef LABSORT_HS_ROT
+#define LABSORT_HS_ROT 1
+#endif
+constexpr bool HS_ROT = LABSORT_HS_ROT != 0;  // rotated flush order per histogram workgroup
 // first position of segment s of an n-key pass input (first active pass)
 __host__ __device__ inline uint32_t seg_start(uint32_t s, size_t n) { return (uint32_t)((size_t)s * n / NSEG); }
 struct SegPlan {
@@ -91,6 +95,9 @@ struct SegPlan {
 constexpr int TS_BLOCK = LABSORT_TS_BLOCK;
 constexpr int TS_KPT = LABSORT_TS_KPT;
 constexpr int TS_TILE = TS_BLOCK * TS_KPT;  // sorted run length of the tile sort
+// key/value tile sort: keys and payloads both in LDS (2 x 64 KB)
+constexpr int TS_KPT_KV = 16;
+constexpr int TS_TILE_KV = TS_BLOCK * TS_KPT_KV;
 
 // ---- merge path ----
 constexpr int MG_BLOCK = 256;
@@ -195,7 +202,9 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t run, uint32_t flip,
-                             uint32_t *part, hipStream_t s);
+                             uint32_t *part, hipStream_t s, const uint32_t *vin = nullptr, uint32_t *vout = nullptr);
+hipError_t launch_tile_sort_kv(const uint32_t *in, uint32_t *out, const uint32_t *vin, uint32_t *vout, size_t n,
+                               uint32_t flip, hipStream_t s);
 hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size_t lb, uint32_t *out, size_t d0,
                            size_t d1, uint32_t flip, uint32_t *part, hipStream_t s);
 hipError_t launch_upper_bound(const uint32_t *keys, size_t n, uint32_t flip, const uint32_t *values, size_t nv,

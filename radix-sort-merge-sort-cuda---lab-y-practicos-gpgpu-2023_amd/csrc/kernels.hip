@@ -355,8 +355,13 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
         for (int q = 0; q < SL; ++q) c += h[i * SL + ((q + i) & (SL - 1))];
         if (c) atomicAdd(&hps[seg * 256 + i], c);
     }
-    // field f = (digit p+1) << 4 | (top nibble of digit p) -> joint[p+1][nibble][digit]
-    for (int i = threadIdx.x; i < 3 * JF; i += HIST_BLOCK) {
+    // field f = (digit p+1) << 4 | (top nibble of digit p) -> joint[p+1][nibble][digit].
+    // Each workgroup starts its flush at a different place (HS_ROT), so the ~12 K
+    // atomics of workgroups that finish together do not queue on the same lines.
+    const uint32_t rot = HS_ROT ? (blockIdx.x * (uint32_t)HIST_BLOCK) % (3u * JF) : 0u;
+    for (int i0 = threadIdx.x; i0 < 3 * JF; i0 += HIST_BLOCK) {
+        int i = i0 + (int)rot;
+        i = i >= 3 * JF ? i - 3 * JF : i;
         const uint32_t c = hj[i];
         const uint32_t p = (uint32_t)i / JF, f = (uint32_t)i % JF;
         if (c) atomicAdd(&joint[((p + 1) * NSEG + (f & 15u)) * 256 + (f >> 4)], c);
@@ -1064,10 +1069,11 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
 // ---------------------------------------------------------------------------------
 // LDS-resident tile sort: 8-bit LSD passes entirely in LDS, one global read and write
 // ---------------------------------------------------------------------------------
-template <int BLOCK, int KPT>
+template <int BLOCK, int KPT, bool KV = false>
 struct TsSmem {
     static constexpr int R = 256, W = BLOCK / WAVE, TILE = BLOCK * KPT;
     uint32_t keys[TILE];
+    uint32_t vals[KV ? TILE : 1];  // key/value: the payload follows its key through every pass
     uint32_t whist[W * R];
     uint32_t dstart[R];
     uint32_t wsum[W];
@@ -1077,9 +1083,12 @@ struct TsSmem {
     uint32_t ordered;
 };
 
-template <int BLOCK, int KPT>
-__global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t flip) {
-    using S = TsSmem<BLOCK, KPT>;
+// KV: key/value pairs (vin/vout, 4-byte payloads); the sort is stable, so equal keys
+// keep their input order and their payloads with them.
+template <int BLOCK, int KPT, bool KV = false>
+__global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint32_t *out, const uint32_t *vin,
+                                                         uint32_t *vout, uint32_t n, uint32_t flip) {
+    using S = TsSmem<BLOCK, KPT, KV>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE;
     __shared__ S sm;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
@@ -1088,8 +1097,16 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
     const uint32_t wbase = base + wid * (KPT * WAVE) + lane;
 
     uint32_t k[KPT];
+    uint32_t v[KV ? KPT : 1];
     uint32_t a = ~0u, o = 0u;
     const bool full = base + (uint32_t)TILE <= n;  // no bounds checks (one base address)
+    if constexpr (KV) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            v[j] = idx < n ? vin[idx] : 0u;
+        }
+    }
     if (full) {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) k[j] = in[wbase + j * WAVE];
@@ -1173,11 +1190,17 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-            sm.keys[sm.dstart[d] + wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = k[j];
+            const uint32_t dst = sm.dstart[d] + wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
+            sm.keys[dst] = k[j];
+            if constexpr (KV) sm.vals[dst] = v[j];
         }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
+        if constexpr (KV) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) v[j] = sm.vals[wid * (KPT * WAVE) + j * WAVE + lane];
+        }
     }
     if (full) {
 #pragma unroll
@@ -1187,6 +1210,13 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
         for (int j = 0; j < KPT; ++j) {
             const uint32_t idx = wbase + j * WAVE;
             if (idx < n) out[idx] = k[j];
+        }
+    }
+    if constexpr (KV) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            if (idx < n) vout[idx] = v[j];
         }
     }
 }
@@ -1234,16 +1264,19 @@ __device__ __forceinline__ uint32_t corank(const uint32_t *A, uint32_t la, const
     return lo;
 }
 
+template <bool KV = false>
 struct MgSmem {
     uint32_t in[MG_TILE];
     uint32_t out[MG_TILE + MG_TILE / 32];
+    uint32_t vin[KV ? MG_TILE : 1];  // key/value: payloads of sm.in
+    uint32_t vout[KV ? MG_TILE + MG_TILE / 32 : 1];
 };
 
 // merge A[a0,a1) and B[b0,b1) (a1-a0 + b1-b0 <= MG_TILE) into out[0 ..)
 template <int BLOCK, int KPT>
 __device__ __forceinline__ void merge_tile(const uint32_t *__restrict__ A, uint32_t a0, uint32_t a1,
                                            const uint32_t *__restrict__ B, uint32_t b0, uint32_t b1,
-                                           uint32_t *__restrict__ out, uint32_t flip, MgSmem &sm) {
+                                           uint32_t *__restrict__ out, uint32_t flip, MgSmem<> &sm) {
     const uint32_t tid = threadIdx.x;
     const uint32_t la = a1 - a0, lb = b1 - b0, tot = la + lb;
     for (uint32_t i = tid; i < la; i += BLOCK) sm.in[i] = A[a0 + i];
@@ -1295,13 +1328,15 @@ __device__ __forceinline__ PairGeom pair_of(uint32_t o, uint32_t n, uint32_t run
 // concurrent binary searches (one per thread, their latencies overlapping; no
 // separate partition launch), then merges tile after tile, the keys of the next
 // tile loading into registers while the current one is merged in LDS.
-template <int BLOCK, int KPT>
+// KV: key/value pairs; each output takes the payload of the key it took (vsrc/vdst).
+template <int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                         uint32_t n, uint32_t run, uint32_t flip, uint32_t ntiles,
-                                                        uint32_t m) {
+                                                        uint32_t m, const uint32_t *__restrict__ vsrc = nullptr,
+                                                        uint32_t *__restrict__ vdst = nullptr) {
     constexpr uint32_t T = (uint32_t)(BLOCK * KPT);
     static_assert(T == (uint32_t)MG_TILE, "tile granularity");
-    __shared__ MgSmem sm;
+    __shared__ MgSmem<KV> sm;
     __shared__ uint32_t s_part[MG_MAX_TPB + 1];
     const uint32_t tid = threadIdx.x;
     const uint32_t t0 = blockIdx.x * m;
@@ -1358,25 +1393,32 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         q.sb = g.pb + g.la + b0;
         return q;
     };
-    auto load = [&](const Geo &q, uint32_t (&v)[KPT]) {
+    auto load = [&](const Geo &q, uint32_t (&v)[KPT], uint32_t (&vv)[KV ? KPT : 1]) {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t k = tid + (uint32_t)j * BLOCK;
-            v[j] = k < q.tot ? src[k < q.la ? q.sa + k : q.sb + (k - q.la)] : 0u;
+            const uint32_t a = k < q.la ? q.sa + k : q.sb + (k - q.la);
+            v[j] = k < q.tot ? src[a] : 0u;
+            if constexpr (KV) vv[j] = k < q.tot ? vsrc[a] : 0u;
         }
     };
     uint32_t nx[KPT];
+    uint32_t nv[KV ? KPT : 1];
     Geo cur = geo(t0);
-    load(cur, nx);
+    load(cur, nx, nv);
     for (uint32_t t = t0; t < t1; ++t) {
         __syncthreads();  // previous tile's merge no longer reads sm.in
 #pragma unroll
         for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
+        if constexpr (KV) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) sm.vin[tid + (uint32_t)j * BLOCK] = nv[j];
+        }
         // next tile: geometry from the co-ranks, keys into registers
         Geo nxt = cur;
         if (t + 1 < t1) {
             nxt = geo(t + 1);
-            load(nxt, nx);
+            load(nxt, nx, nv);
         }
         __syncthreads();  // sm.in holds the current tile
         const uint32_t la = cur.la, lb = cur.tot - cur.la, tot = cur.tot;
@@ -1387,10 +1429,12 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         uint32_t va = ai < la ? sa[ai] : 0u;
         uint32_t vb = bi < lb ? sb[bi] : 0u;
         uint32_t r[KPT];
+        uint32_t from[KV ? KPT : 1];  // key/value: LDS slot (sm.in) of each output
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const bool takeA = (bi >= lb) || (ai < la && key_le(va, vb, flip));
             r[j] = takeA ? va : vb;
+            if constexpr (KV) from[j] = takeA ? ai : la + bi;
             if (takeA) {
                 ++ai;
                 va = ai < la ? sa[ai] : 0u;
@@ -1402,7 +1446,10 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t idx = tid * KPT + j;
-            if (idx < tot) sm.out[idx + (idx >> 5)] = r[j];
+            if (idx < tot) {
+                sm.out[idx + (idx >> 5)] = r[j];
+                if constexpr (KV) sm.vout[idx + (idx >> 5)] = sm.vin[from[j]];
+            }
         }
         __syncthreads();
         uint32_t *__restrict__ o = dst + cur.o0;
@@ -1410,6 +1457,14 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         for (int j = 0; j < KPT; ++j) {
             const uint32_t i = tid + (uint32_t)j * BLOCK;
             if (i < tot) o[i] = sm.out[i + (i >> 5)];
+        }
+        if constexpr (KV) {
+            uint32_t *__restrict__ ov = vdst + cur.o0;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t i = tid + (uint32_t)j * BLOCK;
+                if (i < tot) ov[i] = sm.vout[i + (i >> 5)];
+            }
         }
         cur = nxt;
     }
@@ -1431,7 +1486,7 @@ template <int BLOCK, int KPT>
 __global__ __launch_bounds__(BLOCK) void k_merge_ab(const uint32_t *__restrict__ A, const uint32_t *__restrict__ B,
                                                     uint32_t *__restrict__ out, uint32_t d0, uint32_t d1,
                                                     uint32_t flip, const uint32_t *__restrict__ part) {
-    __shared__ MgSmem sm;
+    __shared__ MgSmem<> sm;
     const uint32_t i = blockIdx.x;
     const uint32_t o0 = d0 + i * (uint32_t)MG_TILE;
     const uint32_t o1 = (d1 - o0) < (uint32_t)MG_TILE ? d1 : o0 + (uint32_t)MG_TILE;
@@ -1608,7 +1663,7 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) 
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const unsigned g = (unsigned)((n + TS_TILE - 1) / TS_TILE);
-    k_tile_sort<TS_BLOCK, TS_KPT><<<g, TS_BLOCK, 0, s>>>(in, out, (uint32_t)n, flip);
+    k_tile_sort<TS_BLOCK, TS_KPT><<<g, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
     return hipGetLastError();
 }
 
@@ -1620,7 +1675,7 @@ hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStr
 }
 
 hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t run, uint32_t flip,
-                             uint32_t *part, hipStream_t s) {
+                             uint32_t *part, hipStream_t s, const uint32_t *vin, uint32_t *vout) {
     if (n == 0) return hipSuccess;
     (void)part;  // co-ranks are found inside k_merge_pass_p
     const uint32_t ntiles = (uint32_t)((n + MG_TILE - 1) / MG_TILE);
@@ -1628,7 +1683,19 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
     uint32_t m = (ntiles + want - 1) / want;  // consecutive tiles per workgroup
     if (m > (uint32_t)MG_MAX_TPB) m = MG_MAX_TPB;
     const uint32_t g = (ntiles + m - 1) / m;
-    k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m);
+    if (vin)
+        k_merge_pass_p<MG_BLOCK, MG_KPT, true>
+            <<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, vin, vout);
+    else
+        k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m);
+    return hipGetLastError();
+}
+
+hipError_t launch_tile_sort_kv(const uint32_t *in, uint32_t *out, const uint32_t *vin, uint32_t *vout, size_t n,
+                               uint32_t flip, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const unsigned g = (unsigned)((n + TS_TILE_KV - 1) / TS_TILE_KV);
+    k_tile_sort<TS_BLOCK, TS_KPT_KV, true><<<g, TS_BLOCK, 0, s>>>(in, out, vin, vout, (uint32_t)n, flip);
     return hipGetLastError();
 }
 

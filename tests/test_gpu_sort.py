@@ -224,6 +224,44 @@ def test_merge_runs_bad_args(ls, torch_gpu):
         ls.merge_runs(t, torch.zeros_like(t), list(range(11)))  # 10 runs > 8
 
 
+# ---- key/value (sort_by_key) ----------------------------------------------------
+@pytest.mark.parametrize("n", [1, 100, 16384, 16385, 100_003, (1 << 20) + 7, 3_000_017])
+@pytest.mark.parametrize("dist,key", [("u32", "u32"), ("mod100", "i32"), ("const", "u32"), ("u32", "i32"),
+                                      ("lowbits", "u32")])
+def test_sort_pairs(ls, oracle, torch_gpu, n, dist, key):
+    """Stable: equal keys keep input order, so the payload (the input index) must equal
+    std::stable_sort's permutation exactly."""
+    torch = torch_gpu
+    k = oracle.gen(n, SEED + 30, dist, param=5)
+    v = np.arange(n, dtype=np.uint32) * np.uint32(2654435761)  # payloads: a bijection of the index
+    ek, ev = oracle.stable_sort_pairs(k, v, key)
+    tk, tv = to_dev(torch, k), to_dev(torch, v)
+    ok, ov = torch.full_like(tk, -1), torch.full_like(tv, -1)
+    ls.sort_pairs_device(tk, tv, ok, ov, n, key=key)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(from_dev(ok), ek)
+    np.testing.assert_array_equal(from_dev(ov), ev)
+    np.testing.assert_array_equal(from_dev(tk), k)  # input untouched
+    # fully in place
+    ls.sort_pairs_device(tk, tv, tk, tv, n, key=key)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(from_dev(tk), ek)
+    np.testing.assert_array_equal(from_dev(tv), ev)
+
+
+def test_sort_pairs_bad_args(ls, torch_gpu):
+    torch = torch_gpu
+    t = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")
+    u = torch.zeros_like(t)
+    o = torch.zeros_like(t)
+    with pytest.raises(ls.LabsortError):
+        ls.sort_pairs_device(t, u, t, o, t.numel())   # keys in place, payloads not
+    with pytest.raises(ls.LabsortError):
+        ls.sort_pairs_device(t, u, o, o, t.numel())   # keys and payloads to one buffer
+    with pytest.raises(ls.LabsortError):
+        ls.sort_pairs_device(t, u, o, t, t.numel(), workspace=torch.zeros(16, dtype=torch.uint8, device="cuda"))
+
+
 # ---- host-pointer drop-ins (lab.h) ------------------------------------------------------------
 @pytest.mark.parametrize("n", [256, 1024, 65536, 1 << 17, 1 << 20])
 def test_order_array_matches_std_sort(ls, oracle, torch_gpu, n):

@@ -200,3 +200,15 @@ def test_restatement_radix_tiles(oracle):
     assert st == "ok"
     for s in range(0, a.size, 32):
         np.testing.assert_array_equal(out[s:s + 32], np.sort(a[s:s + 32]))
+
+
+@pytest.mark.parametrize("key", ["u32", "i32"])
+@pytest.mark.parametrize("dist", ["u32", "mod100", "const"])
+def test_stable_sort_pairs_oracle_vs_numpy(oracle, key, dist):
+    """The sort_by_key oracle (std::stable_sort) against numpy's stable argsort."""
+    k = oracle.gen(50_000, 0x5EED0040, dist, param=3)
+    v = np.arange(k.size, dtype=np.uint32)[::-1].copy()
+    ek, ev = oracle.stable_sort_pairs(k, v, key)
+    order = np.argsort(k.view(np.int32) if key == "i32" else k, kind="stable")
+    np.testing.assert_array_equal(ek, k[order])
+    np.testing.assert_array_equal(ev, v[order])
