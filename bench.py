@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--algo", default="radix", choices=["radix", "merge", "radix1", "pairs"],
                     help="pairs: stable key/value sort (sort_by_key) of (key, uint32 index) pairs")
+    ap.add_argument("--pair-algo", default="radix", choices=["radix", "merge"], help="--algo pairs: which path")
     ap.add_argument("--log2n", type=int, default=28, help="keys per GPU = 2^log2n")
     ap.add_argument("--dist", default="u32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -165,11 +166,11 @@ def main():
         out = torch.empty(n, dtype=torch.int32, device=dev)
         vsrc = torch.arange(n, dtype=torch.int32, device=dev)
         vout = torch.empty(n, dtype=torch.int32, device=dev)
-        ws = torch.empty(max(ls.pairs_workspace_bytes(n), 256), dtype=torch.uint8, device=dev)
+        ws = torch.empty(max(ls.pairs_workspace_bytes(n, args.pair_algo), 256), dtype=torch.uint8, device=dev)
         ls.fill(src, n, SEED + 3, args.dist, stream=stream)
 
         def step():
-            ls.sort_pairs_device(src, vsrc, out, vout, n, key=key, workspace=ws, stream=stream)
+            ls.sort_pairs_device(src, vsrc, out, vout, n, key=key, algo=args.pair_algo, workspace=ws, stream=stream)
             return out
 
         def barrier():
@@ -192,7 +193,8 @@ def main():
         res = step()
     torch.cuda.synchronize()
 
-    dom = "onesweep" if args.algo in ("radix", "radix1") else "merge"
+    dom = "onesweep" if args.algo in ("radix", "radix1") or (args.algo == "pairs" and args.pair_algo == "radix") \
+        else "merge"
     ls.timing_enable(True)
     barrier()
     torch.cuda.synchronize()
@@ -267,7 +269,8 @@ def main():
         traffic, tsrc = pmc_traffic(dom, n)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": traffic, "kernel": ("k_onesweep_p" if dom == "onesweep" and args.algo == "radix" else f"k_{dom}"), "launches": k_cnt,
+                    "traffic": traffic, "kernel": ("k_onesweep_p" if dom == "onesweep" and args.algo == "radix" else
+                               "k_onesweep<8, KV>" if args.algo == "pairs" and dom == "onesweep" else f"k_{dom}"), "launches": k_cnt,
                     "avg_launch_ms": round(avg_ms, 5) if avg_ms else None,
                     "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
         cpu = None
@@ -275,8 +278,9 @@ def main():
             cpu = cpu_baseline(args.cpu_seconds)
         wl = {"radix": "LSD radix sort (8-bit digits, onesweep)", "merge": "LDS tile sort + merge-path passes",
               "radix1": "LSD radix with 1-bit split passes (letra.pdf)",
-              "pairs": "stable key/value sort (uint32 key + uint32 index payload): LDS tile sort + merge-path "
-                       "passes"}[args.algo]
+              "pairs": "stable key/value sort (uint32 key + uint32 index payload): " + (
+                  "8-bit LSD onesweep passes" if args.pair_algo == "radix" else "LDS tile sort + merge-path passes")
+              }[args.algo]
         if world > 1:
             how = ("splitter exchange (pairwise send/recv to all peers at once) + merge tree"
                    if args.exchange == "splitters" else "bitonic pairwise merge-split network")

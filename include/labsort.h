@@ -95,13 +95,16 @@ int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo);
  * Stable sort of n (key, 4-byte payload) pairs: d_keys_in/d_vals_in -> d_keys_out/
  * d_vals_out (out-of-place or fully in place: keys_in == keys_out and vals_in ==
  * vals_out).  Equal keys keep their input order, so sorting (key, index) pairs gives a
- * stable argsort, from which payloads of any width can be gathered.  The merge path
- * with payloads: LDS tile sort of labsort_pair_tile_keys() pairs, then merge-path passes.
- * Asynchronous on `stream`, no allocation; d_ws >= labsort_pairs_workspace_bytes(n). */
+ * stable argsort, from which payloads of any width can be gathered.
+ * algo: LABSORT_ALGO_RADIX (8-bit LSD onesweep passes carrying the payload),
+ * LABSORT_ALGO_MERGE (LDS tile sort of labsort_pair_tile_keys() pairs + merge-path
+ * passes) or LABSORT_ALGO_AUTO (merge up to LABSORT_AUTO_MERGE_MAX_KEYS, radix above).
+ * Asynchronous on `stream`, no allocation; d_ws >= labsort_pairs_workspace_bytes(n, algo). */
 size_t labsort_pair_tile_keys(void);
-size_t labsort_pairs_workspace_bytes(size_t n);
+size_t labsort_pairs_workspace_bytes(size_t n, int algo);
 int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void *d_keys_out, void *d_vals_out,
-                              size_t n, int key_type, void *d_workspace, size_t workspace_bytes, void *stream);
+                              size_t n, int key_type, int algo, void *d_workspace, size_t workspace_bytes,
+                              void *stream);
 
 /* ---- building blocks (exposed for tests and the multi-GPU driver) ---- */
 /* Sort every 64-key tile of d_keys in place by 1-bit splits (ballot + mbcnt +

@@ -90,8 +90,8 @@ def _load() -> ctypes.CDLL:
     L.labsort_pair_tile_keys.restype = sz
     L.labsort_pair_tile_keys.argtypes = []
     L.labsort_pairs_workspace_bytes.restype = sz
-    L.labsort_pairs_workspace_bytes.argtypes = [sz]
-    L.labsort_sort_pairs_device.argtypes = [p, p, p, p, sz, i, p, sz, p]
+    L.labsort_pairs_workspace_bytes.argtypes = [sz, i]
+    L.labsort_sort_pairs_device.argtypes = [p, p, p, p, sz, i, i, p, sz, p]
     L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
     L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
     L.labsort_count_descents.argtypes = [p, sz, i, p, p]
@@ -245,24 +245,25 @@ def merge_runs(d_in, d_out, offsets, key: str = "u32", workspace=None, stream=No
                                   _stream(stream)), "merge_runs")
 
 
-def pairs_workspace_bytes(n: int) -> int:
-    return int(lib.labsort_pairs_workspace_bytes(n))
+def pairs_workspace_bytes(n: int, algo: str = "radix") -> int:
+    return int(lib.labsort_pairs_workspace_bytes(n, ALGO[algo]))
 
 
 def pair_tile_keys() -> int:
     return int(lib.labsort_pair_tile_keys())
 
 
-def sort_pairs_device(d_keys_in, d_vals_in, d_keys_out, d_vals_out, n: int, key: str = "u32", workspace=None,
-                      stream=None) -> None:
+def sort_pairs_device(d_keys_in, d_vals_in, d_keys_out, d_vals_out, n: int, key: str = "u32", algo: str = "radix",
+                      workspace=None, stream=None) -> None:
     """Stable sort of n (key, 4-byte payload) pairs (sort_by_key); equal keys keep
-    their input order.  Asynchronous on `stream`."""
+    their input order.  algo: "radix", "merge" or "auto".  Asynchronous on `stream`."""
     if workspace is None:
         import torch
-        workspace = torch.empty(max(pairs_workspace_bytes(n), 1), dtype=torch.uint8, device="cuda")
+        workspace = torch.empty(max(pairs_workspace_bytes(n, algo), 1), dtype=torch.uint8, device="cuda")
     wsb = workspace.numel() * workspace.element_size()
     _check(lib.labsort_sort_pairs_device(_ptr(d_keys_in), _ptr(d_vals_in), _ptr(d_keys_out), _ptr(d_vals_out), n,
-                                         KEY[key], _ptr(workspace), wsb, _stream(stream)), "sort_pairs_device")
+                                         KEY[key], ALGO[algo], _ptr(workspace), wsb, _stream(stream)),
+           "sort_pairs_device")
 
 
 def histogram(d_keys, n: int, d_hist, bits: int = 8, key: str = "u32", stream=None) -> None:

@@ -452,22 +452,61 @@ int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, i
 
 size_t labsort_pair_tile_keys(void) { return (size_t)TS_TILE_KV; }
 
-size_t labsort_pairs_workspace_bytes(size_t n) {
+size_t labsort_pairs_workspace_bytes(size_t n, int algo) {
     if (n <= (size_t)TS_TILE_KV) return 256;
-    return align_up(n * 4, 256) * 2;  // ping-pong keys | payloads
+    if (algo == LABSORT_ALGO_MERGE) return align_up(n * 4, 256) * 2;  // ping-pong keys | payloads
+    return align_up(radix_layout(n, 8).total, 256) + align_up(n * 4, 256);  // radix workspace | payload ping-pong
 }
 
+namespace {
+// 8-bit LSD radix of (key, payload) pairs: histogram, plan, four onesweep passes
+// (k_onesweep<8, ..., KV>: 8 K-pair tiles, decoupled look-back) and the final copy of
+// keys and payloads, with the same buffer plan for both.
+int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint32_t *vo, size_t n, uint32_t flip,
+                     char *ws, hipStream_t s) {
+    const RadixLayout L = radix_layout(n, 8);
+    Bufs b, vb;
+    b.p[SEL_IN] = const_cast<uint32_t *>(ki);
+    b.p[SEL_OUT] = ko;
+    b.p[SEL_TMP] = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
+    vb.p[SEL_IN] = const_cast<uint32_t *>(vi);
+    vb.p[SEL_OUT] = vo;
+    vb.p[SEL_TMP] = reinterpret_cast<uint32_t *>(ws + align_up(L.total, 256));
+    uint32_t *hist = reinterpret_cast<uint32_t *>(ws + L.off_hist);
+    uint32_t *counters = reinterpret_cast<uint32_t *>(ws + L.off_counter);
+    uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
+    uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
+    Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
+    HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.zero_bytes, s));
+    {
+        TimingScope ts(LABSORT_K_HISTOGRAM, s);
+        HIP_TRY(launch_histogram(ki, n, flip, 8, hist, s));
+    }
+    HIP_TRY(launch_plan(hist, n, 8, ki == ko ? 1 : 0, plan, s));
+    for (int p = 0; p < L.P; ++p) {
+        TimingScope ts(LABSORT_K_ONESWEEP, s);
+        HIP_TRY(launch_onesweep(b, plan, p, 8, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
+                                counters + (size_t)p * OSP_NCTR, err, s, &vb));
+    }
+    HIP_TRY(launch_final_copy(b, plan, n, s));
+    HIP_TRY(launch_final_copy(vb, plan, n, s));
+    return LABSORT_OK;
+}
+}  // namespace
+
 int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void *d_keys_out, void *d_vals_out,
-                              size_t n, int key_type, void *d_ws, size_t ws_bytes, void *stream) {
+                              size_t n, int key_type, int algo, void *d_ws, size_t ws_bytes, void *stream) {
     if (n == 0) return LABSORT_OK;
     if (!d_keys_in || !d_vals_in || !d_keys_out || !d_vals_out) return LABSORT_ERR_ARG;
     if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
-    if (n > 0x7FFFFFFFu) return LABSORT_ERR_ARG;
+    if (algo != LABSORT_ALGO_RADIX && algo != LABSORT_ALGO_MERGE && algo != LABSORT_ALGO_AUTO) return LABSORT_ERR_ARG;
+    if (algo == LABSORT_ALGO_AUTO) algo = n <= (size_t)LABSORT_AUTO_MERGE_MAX_KEYS ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
+    if (n > (algo == LABSORT_ALGO_MERGE ? (size_t)0x7FFFFFFFu : RADIX_MAX_N)) return LABSORT_ERR_ARG;
     // in place only as a whole: one side aliased and the other not would read
     // payloads that the key side's passes already overwrote
     if ((d_keys_in == d_keys_out) != (d_vals_in == d_vals_out)) return LABSORT_ERR_ARG;
     if (d_keys_out == d_vals_out) return LABSORT_ERR_ARG;
-    if (!d_ws || ws_bytes < labsort_pairs_workspace_bytes(n)) return LABSORT_ERR_ARG;
+    if (!d_ws || ws_bytes < labsort_pairs_workspace_bytes(n, algo)) return LABSORT_ERR_ARG;
     const uint32_t flip = flip_of(key_type);
     hipStream_t s = as_stream(stream);
     const uint32_t *ki = static_cast<const uint32_t *>(d_keys_in), *vi = static_cast<const uint32_t *>(d_vals_in);
@@ -477,6 +516,7 @@ int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void
         HIP_TRY(launch_tile_sort_kv(ki, ko, vi, vo, n, flip, s));
         return LABSORT_OK;
     }
+    if (algo == LABSORT_ALGO_RADIX) return sort_pairs_radix(ki, vi, ko, vo, n, flip, static_cast<char *>(d_ws), s);
     // merge passes over runs of TS_TILE_KV pairs, ping-pong between out and the workspace;
     // the tile sort writes where the pass count makes the last pass land in out
     uint32_t *tk = static_cast<uint32_t *>(d_ws);

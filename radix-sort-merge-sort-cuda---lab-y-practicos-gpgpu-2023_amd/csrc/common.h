@@ -198,7 +198,7 @@ hipError_t launch_histogram(const uint32_t *keys, size_t n, uint32_t flip, int b
 hipError_t launch_plan(const uint32_t *hist, size_t n, int bits, int in_is_out, Plan *plan, hipStream_t s);
 hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t n, uint32_t flip,
                            const uint32_t *hist, uint32_t *lookback, uint32_t *counter, uint32_t *err,
-                           hipStream_t s);
+                           hipStream_t s, const Bufs *vb = nullptr);
 hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, uint32_t *joint,
                            hipStream_t s);
 hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, int in_is_out, Plan *plan,

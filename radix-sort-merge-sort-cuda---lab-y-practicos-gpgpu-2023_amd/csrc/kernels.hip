@@ -547,10 +547,11 @@ __global__ __launch_bounds__(256) void k_final_copy(Bufs b, const Plan *__restri
 // ---------------------------------------------------------------------------------
 // one LSD radix pass ("onesweep"): rank, look-back, LDS reorder, coalesced scatter
 // ---------------------------------------------------------------------------------
-template <int BITS, int BLOCK, int KPT>
+template <int BITS, int BLOCK, int KPT, bool KV = false>
 struct OsSmem {
     static constexpr int R = 1 << BITS, W = BLOCK / WAVE, TILE = BLOCK * KPT;
     uint32_t keys[TILE];
+    uint32_t vals[KV ? TILE : 1];  // key/value: payloads reordered with their keys
     uint32_t whist[W * R];
     uint32_t gscan[R];
     uint32_t dstart[R];
@@ -562,11 +563,15 @@ struct OsSmem {
 
 constexpr uint32_t SPIN_LIMIT = 1u << 22;
 
-template <int BITS, int BLOCK, int KPT>
+// KV: key/value pairs; vbufs holds the payload buffers (IN, OUT, TMP) that the plan
+// selects exactly as for the keys, and each payload is reordered and scattered with
+// its key (stable, like the keys).
+template <int BITS, int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n,
                                                     uint32_t flip, const uint32_t *__restrict__ ghist,
-                                                    uint32_t *lookback, uint32_t *counter, uint32_t *err) {
-    using S = OsSmem<BITS, BLOCK, KPT>;
+                                                    uint32_t *lookback, uint32_t *counter, uint32_t *err,
+                                                    Bufs vbufs) {
+    using S = OsSmem<BITS, BLOCK, KPT, KV>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE;
     constexpr uint32_t RM = R - 1;
     static_assert(R <= BLOCK, "one thread per digit");
@@ -603,6 +608,15 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
             k[j] = idx < n ? in[idx] : sentinel;
         }
     }
+    uint32_t v[KV ? KPT : 1];
+    if constexpr (KV) {
+        const uint32_t *__restrict__ vin = vbufs.p[srcsel];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            v[j] = idx < n ? vin[idx] : 0u;
+        }
+    }
     uint32_t dig[KPT], rank[KPT];
 #pragma unroll
     for (int j = 0; j < KPT; ++j) dig[j] = ((k[j] ^ flip) >> shift) & RM;
@@ -629,7 +643,11 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
 
     // reorder the tile by digit in LDS
 #pragma unroll
-    for (int j = 0; j < KPT; ++j) sm.keys[sm.dstart[dig[j]] + wh[dig[j]] + rank[j]] = k[j];
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t pos = sm.dstart[dig[j]] + wh[dig[j]] + rank[j];
+        sm.keys[pos] = k[j];
+        if constexpr (KV) sm.vals[pos] = v[j];
+    }
 
     // decoupled look-back: exclusive count of my digit in all earlier tiles
     if (tid < (uint32_t)R) {
@@ -664,6 +682,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
             const uint32_t key = sm.keys[i];
             const uint32_t d = ((key ^ flip) >> shift) & RM;
             out[sm.delta[d] + i] = key;
+            if constexpr (KV) vbufs.p[plan->dst[pass]][sm.delta[d] + i] = sm.vals[i];
         }
     }
 }
@@ -1568,14 +1587,19 @@ hipError_t launch_plan(const uint32_t *hist, size_t n, int bits, int in_is_out, 
 
 hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t n, uint32_t flip,
                            const uint32_t *hist, uint32_t *lookback, uint32_t *counter, uint32_t *err,
-                           hipStream_t s) {
+                           hipStream_t s, const Bufs *vb) {
     const unsigned g = (unsigned)((n + OS_TILE - 1) / OS_TILE);
-    if (bits == 8)
+    if (vb && bits == 8)
+        k_onesweep<8, OS_BLOCK, OS_KPT, true><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist,
+                                                                     lookback, counter, err, *vb);
+    else if (vb)
+        return hipErrorInvalidValue;
+    else if (bits == 8)
         k_onesweep<8, OS_BLOCK, OS_KPT><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback,
-                                                               counter, err);
+                                                               counter, err, Bufs{});
     else if (bits == 1)
         k_onesweep<1, OS_BLOCK, OS_KPT><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback,
-                                                               counter, err);
+                                                               counter, err, Bufs{});
     else return hipErrorInvalidValue;
     return hipGetLastError();
 }

@@ -225,10 +225,11 @@ def test_merge_runs_bad_args(ls, torch_gpu):
 
 
 # ---- key/value (sort_by_key) ----------------------------------------------------
+@pytest.mark.parametrize("algo", ["radix", "merge"])
 @pytest.mark.parametrize("n", [1, 100, 16384, 16385, 100_003, (1 << 20) + 7, 3_000_017])
 @pytest.mark.parametrize("dist,key", [("u32", "u32"), ("mod100", "i32"), ("const", "u32"), ("u32", "i32"),
                                       ("lowbits", "u32")])
-def test_sort_pairs(ls, oracle, torch_gpu, n, dist, key):
+def test_sort_pairs(ls, oracle, torch_gpu, n, dist, key, algo):
     """Stable: equal keys keep input order, so the payload (the input index) must equal
     std::stable_sort's permutation exactly."""
     torch = torch_gpu
@@ -237,13 +238,13 @@ def test_sort_pairs(ls, oracle, torch_gpu, n, dist, key):
     ek, ev = oracle.stable_sort_pairs(k, v, key)
     tk, tv = to_dev(torch, k), to_dev(torch, v)
     ok, ov = torch.full_like(tk, -1), torch.full_like(tv, -1)
-    ls.sort_pairs_device(tk, tv, ok, ov, n, key=key)
+    ls.sort_pairs_device(tk, tv, ok, ov, n, key=key, algo=algo)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(from_dev(ok), ek)
     np.testing.assert_array_equal(from_dev(ov), ev)
     np.testing.assert_array_equal(from_dev(tk), k)  # input untouched
     # fully in place
-    ls.sort_pairs_device(tk, tv, tk, tv, n, key=key)
+    ls.sort_pairs_device(tk, tv, tk, tv, n, key=key, algo=algo)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(from_dev(tk), ek)
     np.testing.assert_array_equal(from_dev(tv), ev)
