@@ -21,7 +21,7 @@ shard (one all_gather), cut their sorted shards at the splitters
 (`labsort_upper_bound`), send piece j to rank j with pairwise send/recv posted to
 all peers at once (so all 7 xGMI links of a node carry data together instead of
 one per step) straight into one buffer, and merge the p received runs in rank
-order (a tree of `labsort_merge` passes, or one K-way `labsort_merge_runs` pass;
+order in one K-way `labsort_merge_runs` pass (or a tree of `labsort_merge` passes;
 A before B on ties).  Rank r then holds the r-th contiguous
 range of the sorted array; range sizes follow the splitters (within a few percent
 of n/p on varied data; skewed data with a heavy repeated key can unbalance them).
@@ -86,12 +86,12 @@ class Ops:
 class HipOps(Ops):
     """liblabsort.so on the current GPU."""
 
-    def __init__(self, ls, key: str = "u32", local_algo: str = "radix", stream=None, kway: bool = False):
+    def __init__(self, ls, key: str = "u32", local_algo: str = "radix", stream=None, kway: bool = True):
         self.ls, self.key, self.algo, self.stream = ls, key, local_algo, stream
         # kway: merge the received runs in one K-way pass (labsort_merge_runs) instead of
-        # the tree of pairwise merge-path passes.  Off by default: on MI355X the tree is
-        # faster (one pairwise pass 0.51 ms vs an 8-way pass ~1.9 ms at 2^28, r15;
-        # the K-way block merge is bound by LDS operations, DESIGN.md section 3.2)
+        # a tree of labsort_merge calls.  Measured on MI355X for 2^28 keys in p runs
+        # (profiles/r15_dist_merge_step.jsonl): p = 2 / 4 / 8: K-way 0.62 / 1.24 /
+        # 1.91 ms, tree 0.75 / 1.47 / 2.28 ms
         self.kway = kway
         self._ws = None
         self._part = None
@@ -117,8 +117,8 @@ class HipOps(Ops):
         return out[: d1 - d0]
 
     def merge_runs(self, buf, offsets):
-        """One K-way pass (labsort_merge_runs, K <= 8) when self.kway; otherwise (and for
-        more than 8 runs) the merge tree."""
+        """One K-way pass (labsort_merge_runs, K <= 8) when self.kway (the default);
+        otherwise, and for more than 8 runs, the merge tree."""
         if not self.kway or len(offsets) - 1 > 8:
             return super().merge_runs(buf, offsets)
         n = offsets[-1] - offsets[0]
