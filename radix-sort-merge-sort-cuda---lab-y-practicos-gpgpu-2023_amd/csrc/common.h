@@ -113,6 +113,11 @@ constexpr int MG_BLOCK = LABSORT_MG_BLOCK;  // r15 sweep: 512 x 8 keys (4096-key
 constexpr int MG_KPT = LABSORT_MG_KPT;
 constexpr int MG_TILE = MG_BLOCK * MG_KPT;
 constexpr int MG_MAX_TPB = 256;       // most consecutive output tiles per merge workgroup
+constexpr int MG_MAX_PAIRS = 4;       // explicit pairs of runs per merge level (up to 8 runs)
+struct MgPairs {
+    uint32_t np;  // 0: uniform runs
+    uint32_t pb[MG_MAX_PAIRS + 1], pm[MG_MAX_PAIRS], tpre[MG_MAX_PAIRS + 1];
+};
 #ifndef LABSORT_MG_BRACKET
 #define LABSORT_MG_BRACKET 8
 #endif
