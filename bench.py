@@ -53,7 +53,8 @@ def parse():
     ap.add_argument("--log2n", type=int, default=28, help="keys per GPU = 2^log2n")
     ap.add_argument("--dist", default="u32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample")
+    ap.add_argument("--no-merge", action="store_true", help="skip the merge-sort leg (config 4) of the N=1 radix run")
+    ap.add_argument("--cpu-seconds", type=float, default=16.0, help="budget of the CPU baseline samples")
     ap.add_argument("--exchange", default="splitters", choices=["splitters", "pairwise"],
                     help="N>1: all-peer splitter exchange + merge tree, or the bitonic pairwise merge-split network")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -98,23 +99,67 @@ def verify(torch, ls, src, out, n, key):
     return ok, int(cnt.item())
 
 
-def cpu_baseline(budget_s: float):
-    """std::sort (oracle/cpu_sort.cpp) on 1 core over samples of the same workload:
-    uniform uint32 keys from the same generator, 2^24 keys per sort, repeated until
-    the budget is spent.  Reported as Mkeys/s."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_threads() -> int:
+    """Host threads this process may use: its CPU affinity, capped by OMP_NUM_THREADS
+    (the GPU box gives one GPU's job a 16-thread share of a larger machine)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(omp))) if omp and omp.isdigit() else aff
+
+
+def cpu_baseline(budget_s: float, n: int, ls):
+    """CPU sorts of the same workload (uniform uint32 keys from the same generator,
+    seed 0x5EED0003) on the host cores of the GPU box, as SURVEY §8(d) lists them:
+      std::sort            1 core, 2^24-key samples repeated for ~budget_s/2 (the headline)
+      __gnu_parallel::sort all usable threads, the full n, 2 repetitions
+      thrust::sort (host)  the reference's "Trust" column (lab.cu:404-406): rocThrust's
+                           sequential host radix sort on an int* buffer, 1 core, 2^24 samples
+    All Mkeys/s.  `value` is std::sort: the oracle (kind "port")."""
+    import numpy as np
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O  # test infrastructure: the CPU baseline leg only
 
     ns = 1 << 24
     keys = O.gen(ns, SEED + 3, "u32")
-    t = 0.0
-    reps = 0
-    while t < budget_s and reps < 64:
+    t, reps = 0.0, 0
+    while t < budget_s / 2 and reps < 64:
         t += O.time_sort_u32(keys, threads=1, reps=1)
         reps += 1
+    thr = cpu_threads()
+    full = O.gen(n, SEED + 3, "u32")
+    tp = O.time_sort_u32(full, threads=thr, reps=2) / 2
+    del full
+    tt, treps = 0.0, 0
+    while tt < budget_s / 4 and treps < 64:
+        buf = keys.view(np.int32).copy()
+        t0 = time.perf_counter()
+        ls.order_with_trust(buf)
+        tt += time.perf_counter() - t0
+        treps += 1
     return {"value": round(ns * reps / t / 1e6, 2), "unit": "Mkeys/s", "cores": 1, "kind": "port",
             "sample": f"std::sort of {reps} x 2^24 uniform uint32 keys (same generator, seed 0x5EED0003), "
-                      f"{t:.1f} s on one host core"}
+                      f"{t:.1f} s on one host core",
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "parallel": {"value": round(n / tp / 1e6, 2), "unit": "Mkeys/s", "cores": thr,
+                         "sample": f"__gnu_parallel::sort of the full 2^{n.bit_length() - 1} keys, "
+                                   f"{thr} threads, mean of 2 ({tp:.2f} s each)"},
+            "thrust_host": {"value": round(ns * treps / tt / 1e6, 2), "unit": "Mkeys/s", "cores": 1,
+                            "sample": f"rocThrust thrust::sort on a host int* (order_with_trust, lab.cu:404), "
+                                      f"{treps} x 2^24 keys, {tt:.1f} s"}}
 
 
 def main():
@@ -188,13 +233,26 @@ def main():
         def barrier():
             pass
 
+    def status():
+        """the kernels' own error report for the last sort (raises LabsortError)"""
+        if world > 1:
+            return  # HipOps.local_sort checks it after every local sort
+        if args.algo == "pairs":
+            ls.pairs_workspace_status(ws, n, args.pair_algo, stream=stream)
+        else:
+            ls.workspace_status(ws, n, args.algo, stream=stream)
+
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         res = step()
     torch.cuda.synchronize()
+    status()
 
     dom = "onesweep" if args.algo in ("radix", "radix1") or (args.algo == "pairs" and args.pair_algo == "radix") \
         else "merge"
+    if world > 1:
+        comm.sent_bytes, comm.p2p_rounds, comm.exchange_s = 0, 0, 0.0
+        comm.timed = True
     ls.timing_enable(True)
     barrier()
     torch.cuda.synchronize()
@@ -207,6 +265,7 @@ def main():
     k_ms, k_cnt = ls.timing_read(dom)
     ls.timing_enable(False)
     elapsed = t1 - t0
+    status()
 
     if world > 1:
         import torch.distributed as dist
@@ -258,9 +317,72 @@ def main():
               file=sys.stderr)
         sys.exit(3)
 
+    # config 4 beside the headline: the merge sort of the same device input (N = 1,
+    # radix headline only); its own verification, status check and kernel timings
+    merge_leg = None
+    if world == 1 and args.algo == "radix" and not args.no_merge:
+        mws = torch.empty(max(ls.workspace_bytes(n, "merge"), 256), dtype=torch.uint8, device=dev)
+        mout = torch.empty_like(src)
+
+        def mstep():
+            ls.sort_device(src, mout, n, key=key, algo="merge", workspace=mws, stream=stream)
+
+        for _ in range(args.warmup):
+            mstep()
+        torch.cuda.synchronize()
+        ls.timing_enable(True)
+        m0 = time.perf_counter()
+        for _ in range(args.steps):
+            mstep()
+        torch.cuda.synchronize()
+        m1 = time.perf_counter()
+        mp_ms, mp_cnt = ls.timing_read("merge")
+        ts_ms, ts_cnt = ls.timing_read("tile_sort")
+        ls.timing_enable(False)
+        ls.workspace_status(mws, n, "merge", stream=stream)
+        mok, _ = verify(torch, ls, src, mout, n, key)
+        if not mok:
+            print("bench.py: MERGE OUTPUT CHECK FAILED", file=sys.stderr)
+            sys.exit(3)
+        mavg = mp_ms / mp_cnt if mp_cnt else None
+        tavg = ts_ms / ts_cnt if ts_cnt else None
+        mtraffic, msrc = pmc_traffic("merge", n)
+        ttraffic, _ = pmc_traffic("tile_sort", n)
+        merge_leg = {
+            "workload": f"LDS tile sort + merge-path passes of the same 2^{args.log2n} device-resident keys "
+                        "(BASELINE config 4)",
+            "value": round(n * args.steps / (m1 - m0) / 1e6, 2), "unit": "Mkeys/s",
+            "ms_per_step": round((m1 - m0) / args.steps * 1e3, 4), "passes_per_sort": mp_cnt // max(args.steps, 1),
+            "verified": "sorted permutation (descents, digit histograms, sums)",
+            "roofline": {"bound": "hbm", "kernel": "k_merge_pass_p", "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "avg_launch_ms": round(mavg, 5) if mavg else None,
+                         "achieved": round(8.0 * n / (mavg * 1e-3) / 1e9, 1) if mavg else None,
+                         "frac": round(8.0 * n / (mavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if mavg else None,
+                         "algorithmic_bytes_per_launch": 8.0 * n, "traffic": mtraffic, "traffic_source": msrc},
+            "tile_sort": {"kernel": "k_tile_sort", "avg_launch_ms": round(tavg, 5) if tavg else None,
+                          "achieved": round(8.0 * n / (tavg * 1e-3) / 1e9, 1) if tavg else None,
+                          "frac": round(8.0 * n / (tavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tavg else None,
+                          "traffic": ttraffic},
+        }
+        del mws, mout
+
     total_keys = n * world * args.steps
     value = total_keys / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
+    xgmi = None
+    if world > 1:
+        import torch.distributed as dist
+        st = torch.tensor([comm.sent_bytes, comm.exchange_s * 1e9, comm.p2p_rounds], dtype=torch.float64,
+                          device=cdev)
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+        sent, exs, rounds = float(st[0]) / args.steps, float(st[1]) / 1e9 / args.steps, float(st[2]) / args.steps
+        links = world - 1 if args.exchange == "splitters" else 1
+        xgmi = {"bytes_sent_per_rank_per_step": int(sent), "p2p_rounds_per_step": rounds,
+                "exchange_ms_per_step": round(exs * 1e3, 4),
+                "links_per_round": links,
+                "per_link_GBps": round(sent / links / exs / 1e9, 2) if exs > 0 else None,
+                "note": "max over ranks; exchange time is host wall time around the point-to-point calls "
+                        "(stream synchronised on both sides)"}
 
     if rank == 0:
         avg_ms = k_ms / k_cnt if k_cnt else None
@@ -275,7 +397,7 @@ def main():
                     "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_seconds)
+            cpu = cpu_baseline(args.cpu_seconds, n, ls)
         wl = {"radix": "LSD radix sort (8-bit digits, onesweep)", "merge": "LDS tile sort + merge-path passes",
               "radix1": "LSD radix with 1-bit split passes (letra.pdf)",
               "pairs": "stable key/value sort (uint32 key + uint32 index payload): " + (
@@ -301,6 +423,11 @@ def main():
                 "; payloads gather the output keys, stable" if args.algo == "pairs" and world == 1 else ""),
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if merge_leg:
+            line["merge"] = merge_leg
+        if xgmi:
+            line["config"]["local_algo"] = "radix"
+            line["xgmi"] = xgmi
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

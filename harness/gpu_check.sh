@@ -13,7 +13,7 @@ run() { echo "== $(date +%T) $*" | tee -a "$O/steps.log"; }
 ok=0
 if [[ "$STEPS" == all || "$STEPS" == *tests* ]]; then
   run pytest
-  timeout -k 10 900 python -m pytest "$R/tests" -m gpu -x -q -p no:cacheprovider > "$O/pytest_gpu.log" 2>&1 || { echo "pytest failed"; tail -30 "$O/pytest_gpu.log"; exit 1; }
+  timeout -k 10 ${PYTEST_LIMIT:-900} python -u -m pytest "$R/tests" -m gpu -x -v --timeout 150 --timeout-method thread -p no:cacheprovider ${PYTEST_ARGS:-} > "$O/pytest_gpu.log" 2>&1 || { echo "pytest failed"; tail -40 "$O/pytest_gpu.log"; exit 1; }
   tail -3 "$O/pytest_gpu.log"
   run smoke
   timeout -k 10 300 python -c "import sys; sys.path.insert(0,'$R'); import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || { cat "$O/smoke.log"; exit 1; }
@@ -23,9 +23,6 @@ if [[ "$STEPS" == all || "$STEPS" == *bench* ]]; then
   run bench
   timeout -k 10 400 python "$R/bench.py" > "$O/bench_$TAG.json" 2> "$O/bench_$TAG.err" || { cat "$O/bench_$TAG.err"; exit 1; }
   cat "$O/bench_$TAG.json"
-  run bench merge
-  timeout -k 10 400 python "$R/bench.py" --algo merge --no-cpu-baseline > "$O/bench_merge_$TAG.json" 2> "$O/bench_merge_$TAG.err" || { cat "$O/bench_merge_$TAG.err"; exit 1; }
-  cat "$O/bench_merge_$TAG.json"
 fi
 if [[ "$STEPS" == all || "$STEPS" == *prof* ]]; then
   run rocprof stats

@@ -87,8 +87,19 @@ size_t labsort_workspace_bytes(size_t n, int algo);
  * Asynchronous on `stream`; no host synchronisation, graph-capturable. */
 int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, int algo, void *d_workspace,
                         size_t workspace_bytes, void *stream);
-/* Host pointer in/out, synchronous: the order_array contract (lab.cu:303). */
+/* Host pointer in/out, synchronous: the order_array contract (lab.cu:303).
+ * Returns LABSORT_ERR_DEVICE when a kernel reported an internal error. */
 int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo);
+/* Device-side status of the last labsort_sort_device(n, algo) that used d_workspace:
+ * synchronises `stream`, then returns LABSORT_ERR_DEVICE if a kernel of that sort set
+ * the workspace's error word (a bounded look-back spin expired: the result is not
+ * valid), else LABSORT_OK.  The error word is the first 32-bit word of a radix
+ * workspace, cleared at the start of every radix sort; merge-path sorts have none and
+ * report LABSORT_OK.  The reference's policy (CUDA_CHK after every launch, utils.h:18-26)
+ * checks launch status only; this adds the kernels' own failure report. */
+int labsort_workspace_status(const void *d_workspace, size_t n, int algo, void *stream);
+/* The same for the last labsort_sort_pairs_device(n, algo) on d_workspace. */
+int labsort_pairs_workspace_status(const void *d_workspace, size_t n, int algo, void *stream);
 
 /* ---- key/value (sort_by_key; no lab.cu counterpart, the reference sorts
  * keys only) ----

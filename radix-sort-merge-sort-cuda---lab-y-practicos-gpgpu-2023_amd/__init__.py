@@ -41,6 +41,7 @@ C_SYMBOLS = [
     "labsort_count_descents", "labsort_timing_enable", "labsort_timing_read", "labsort_upper_bound", "sort",
     "labsort_merge_runs_workspace_bytes", "labsort_merge_runs",
     "labsort_pair_tile_keys", "labsort_pairs_workspace_bytes", "labsort_sort_pairs_device",
+    "labsort_workspace_status", "labsort_pairs_workspace_status",
 ]
 CXX_SYMBOLS = ["_Z11order_arrayPii", "_Z16order_with_trustPii"]
 
@@ -92,6 +93,8 @@ def _load() -> ctypes.CDLL:
     L.labsort_pairs_workspace_bytes.restype = sz
     L.labsort_pairs_workspace_bytes.argtypes = [sz, i]
     L.labsort_sort_pairs_device.argtypes = [p, p, p, p, sz, i, i, p, sz, p]
+    L.labsort_workspace_status.argtypes = [p, sz, i, p]
+    L.labsort_pairs_workspace_status.argtypes = [p, sz, i, p]
     L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
     L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
     L.labsort_count_descents.argtypes = [p, sz, i, p, p]
@@ -200,14 +203,33 @@ def merge_parts(n: int) -> int:
 
 def sort_device(d_in, d_out, n: int, key: str = "u32", algo: str = "radix", workspace=None,
                 workspace_bytes_: int | None = None, stream=None) -> None:
-    """Sort n keys d_in -> d_out (may alias) asynchronously on `stream`."""
-    if workspace is None:
+    """Sort n keys d_in -> d_out (may alias) asynchronously on `stream`.
+
+    With a caller-owned `workspace` the call stays asynchronous; check the kernels'
+    own error report with workspace_status() once the result is needed.  Without
+    one, the call allocates a workspace, synchronises and checks it itself."""
+    own = workspace is None
+    if own:
         import torch
         workspace = torch.empty(max(workspace_bytes(n, algo), 1), dtype=torch.uint8, device="cuda")
     wsb = workspace_bytes_ if workspace_bytes_ is not None else (
         workspace.numel() * workspace.element_size() if hasattr(workspace, "numel") else workspace_bytes(n, algo))
     _check(lib.labsort_sort_device(_ptr(d_in), _ptr(d_out), n, KEY[key], ALGO[algo], _ptr(workspace), wsb,
                                    _stream(stream)), "sort_device")
+    if own:
+        workspace_status(workspace, n, algo, stream)
+
+
+def workspace_status(workspace, n: int, algo: str = "radix", stream=None) -> None:
+    """Synchronise `stream` and raise LabsortError(device-side error) if a kernel of the
+    last sort_device(n, algo) on `workspace` reported a failure (labsort_workspace_status)."""
+    _check(lib.labsort_workspace_status(_ptr(workspace), n, ALGO[algo], _stream(stream)), "sort_device (status)")
+
+
+def pairs_workspace_status(workspace, n: int, algo: str = "radix", stream=None) -> None:
+    """As workspace_status, for the last sort_pairs_device(n, algo) on `workspace`."""
+    _check(lib.labsort_pairs_workspace_status(_ptr(workspace), n, ALGO[algo], _stream(stream)),
+           "sort_pairs_device (status)")
 
 
 def wave_tile_sort(d_keys, n: int, key: str = "u32", stream=None) -> None:
@@ -257,13 +279,16 @@ def sort_pairs_device(d_keys_in, d_vals_in, d_keys_out, d_vals_out, n: int, key:
                       workspace=None, stream=None) -> None:
     """Stable sort of n (key, 4-byte payload) pairs (sort_by_key); equal keys keep
     their input order.  algo: "radix", "merge" or "auto".  Asynchronous on `stream`."""
-    if workspace is None:
+    own = workspace is None
+    if own:
         import torch
         workspace = torch.empty(max(pairs_workspace_bytes(n, algo), 1), dtype=torch.uint8, device="cuda")
     wsb = workspace.numel() * workspace.element_size()
     _check(lib.labsort_sort_pairs_device(_ptr(d_keys_in), _ptr(d_vals_in), _ptr(d_keys_out), _ptr(d_vals_out), n,
                                          KEY[key], ALGO[algo], _ptr(workspace), wsb, _stream(stream)),
            "sort_pairs_device")
+    if own:
+        pairs_workspace_status(workspace, n, algo, stream)
 
 
 def histogram(d_keys, n: int, d_hist, bits: int = 8, key: str = "u32", stream=None) -> None:

@@ -99,10 +99,11 @@ RadixLayout radix_layout(size_t n, int bits) {
     L.R = 1 << bits;
     L.P = (32 + bits - 1) / bits;
     L.ntiles = (n + OS_TILE - 1) / OS_TILE + (bits == 8 ? NSEG : 0);
+    // zeroed block: err | hist | segment histograms | counters | lookback.  The device
+    // error word is the workspace's first word (labsort_workspace_status reads it).
     size_t o = 0;
-    L.off_tmp = o;
-    o = align_up(o + n * 4, 256);
-    // zeroed block: hist | segment histograms | counters | err | lookback (one memset per sort)
+    L.off_err = o;
+    o += 256;
     L.off_hist = o;
     o += (size_t)L.P * L.R * 4;
     L.off_hps = o;
@@ -111,18 +112,18 @@ RadixLayout radix_layout(size_t n, int bits) {
     if (bits == 8) o += (size_t)4 * NSEG * 256 * 4;
     L.off_counter = o;
     o += (size_t)L.P * OSP_NCTR * 4;
-    L.off_err = o;
-    o += 16;
     o = align_up(o, 256);
     L.off_lookback = o;
     o += (size_t)L.P * L.ntiles * L.R * 4;
     o = align_up(o, 256);
-    L.zero_bytes = o - L.off_hist;
+    L.zero_bytes = o;
     L.off_plan = o;
     o = align_up(o + sizeof(Plan), 256);
     L.off_segplan = o;
     if (bits == 8) o = align_up(o + 4 * sizeof(SegPlan), 256);
-    L.total = o;
+    // the ping-pong key buffer last, 64 KiB aligned (tiles are 64 KiB of keys)
+    L.off_tmp = align_up(o, 65536);
+    L.total = align_up(L.off_tmp + n * 4, 256);
     return L;
 }
 
@@ -158,7 +159,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
     if (bits == 8) {
         // histograms first; the look-back words (tens of MB) are cleared after the
         // histogram so their dirty lines do not compete with its read of the keys
-        HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.off_lookback - L.off_hist, s));
+        HIP_TRY(hipMemsetAsync(ws, 0, L.off_lookback, s));
         uint32_t *hps = reinterpret_cast<uint32_t *>(ws + L.off_hps);
         uint32_t *joint = reinterpret_cast<uint32_t *>(ws + L.off_joint);
         SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
@@ -166,7 +167,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
             HIP_TRY(launch_hist_seg(in, n, flip, hps, joint, s));
         }
-        HIP_TRY(hipMemsetAsync(ws + L.off_lookback, 0, L.off_hist + L.zero_bytes - L.off_lookback, s));
+        HIP_TRY(hipMemsetAsync(ws + L.off_lookback, 0, L.zero_bytes - L.off_lookback, s));
         HIP_TRY(launch_plan8(hps, joint, n, in == out ? 1 : 0, plan, sps, hist, s));
         for (int p = 0; p < L.P; ++p) {
             if (p > 0) HIP_TRY(launch_segplan(plan, p, n, hist, joint, sps, s));
@@ -175,7 +176,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
                                       counters + (size_t)p * OSP_NCTR, err, s));
         }
     } else {
-        HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.zero_bytes, s));
+        HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes, s));
         {
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
             HIP_TRY(launch_histogram(in, n, flip, bits, hist, s));
@@ -286,6 +287,49 @@ int resolve_algo(int algo, size_t n) {
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------
+// LABSORT_VERIFY=1: every host-pointer drop-in call (order_array / sort /
+// order_with_trust) checks its own result -- no descents in int32 order, and the
+// same multiset as the input (sum, sum of squares and xor of a mixed hash, all mod
+// 2^64) -- prints "labsort-verify,<caller>,<n>,ok" on stderr, and on a mismatch
+// fails with the reference's error policy (GPUassert line + exit, utils.h:18-26).
+// This is the harness's verify column without editing main.cpp.
+// ---------------------------------------------------------------------------------
+namespace labsort {
+static inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+bool verify_enabled() {
+    const char *e = std::getenv("LABSORT_VERIFY");
+    return e && *e && std::strcmp(e, "0") != 0;
+}
+KeyPrint key_print(const int *a, size_t n) {
+    KeyPrint p{0, 0, 0};
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t v = (uint32_t)a[i];
+        p.s1 += v;
+        p.s2 += v * v;
+        p.x ^= mix64(v + 0x9E3779B97F4A7C15ull);
+    }
+    return p;
+}
+void verify_or_exit(const char *who, const int *a, size_t n, const KeyPrint &before) {
+    size_t desc = 0;
+    for (size_t i = 1; i < n; ++i) desc += a[i - 1] > a[i];
+    const KeyPrint after = key_print(a, n);
+    const bool perm = after.s1 == before.s1 && after.s2 == before.s2 && after.x == before.x;
+    if (desc || !perm) {
+        std::fprintf(stderr, "GPUassert: labsort verify failed in %s: n=%zu, %zu descents, %s %s %d\n", who, n, desc,
+                     perm ? "same multiset" : "NOT a permutation of the input", __FILE__, __LINE__);
+        std::exit(1);
+    }
+    std::fprintf(stderr, "labsort-verify,%s,%zu,ok\n", who, n);
+}
+}  // namespace labsort
+
+
 // =================================================================================
 // C-ABI
 // =================================================================================
@@ -350,6 +394,31 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
     return sort_radix(in, out, n, flip, algo == LABSORT_ALGO_RADIX1 ? 1 : 8, ws, s);
 }
 
+namespace {
+// Synchronise the stream, then read the device error word (the workspace's first
+// word) when the sort that used the workspace had a radix layout.
+int read_status(const void *d_ws, bool radix_layout_used, hipStream_t s) {
+    HIP_TRY(hipStreamSynchronize(s));
+    if (!radix_layout_used) return LABSORT_OK;
+    if (!d_ws) return LABSORT_ERR_ARG;
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, d_ws, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return err ? LABSORT_ERR_DEVICE : LABSORT_OK;
+}
+}  // namespace
+
+int labsort_workspace_status(const void *d_ws, size_t n, int algo, void *stream) {
+    if (n == 0) return read_status(d_ws, false, as_stream(stream));
+    algo = resolve_algo(algo, n);
+    return read_status(d_ws, !small_path(n, algo) && algo != LABSORT_ALGO_MERGE, as_stream(stream));
+}
+
+int labsort_pairs_workspace_status(const void *d_ws, size_t n, int algo, void *stream) {
+    if (algo == LABSORT_ALGO_AUTO) algo = n <= (size_t)LABSORT_AUTO_MERGE_MAX_KEYS ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
+    return read_status(d_ws, n > (size_t)TS_TILE_KV && algo == LABSORT_ALGO_RADIX, as_stream(stream));
+}
+
 int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo) {
     if (n == 0) return LABSORT_OK;
     if (!h_keys) return LABSORT_ERR_ARG;
@@ -370,14 +439,7 @@ int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo) {
     st = labsort_sort_device(c.keys, c.keys, n, key_type, algo, c.ws, c.ws_bytes, c.stream);
     if (st) return st;
     HIP_TRY(hipMemcpyAsync(h_keys, c.keys, n * 4, hipMemcpyDeviceToHost, c.stream));
-    HIP_TRY(hipStreamSynchronize(c.stream));
-    if (!small_path(n, algo) && algo != LABSORT_ALGO_MERGE) {
-        const RadixLayout L = radix_layout(n, algo == LABSORT_ALGO_RADIX1 ? 1 : 8);
-        uint32_t err = 0;
-        HIP_TRY(hipMemcpy(&err, static_cast<char *>(c.ws) + L.off_err, 4, hipMemcpyDeviceToHost));
-        if (err) return LABSORT_ERR_DEVICE;
-    }
-    return LABSORT_OK;
+    return labsort_workspace_status(c.ws, n, algo, c.stream);
 }
 
 int labsort_wave_tile_sort(void *d_keys, size_t n, int key_type, void *stream) {
@@ -596,6 +658,9 @@ int labsort_timing_read(int cls, double *total_ms, long long *launches) {
 
 void sort(int *in, int n) {
     if (n <= 0) return;
+    const bool verify = verify_enabled();
+    KeyPrint before{};
+    if (verify) before = key_print(in, (size_t)n);
     const int st = labsort_sort_host(in, (size_t)n, LABSORT_KEY_I32, default_algo());
     if (st != LABSORT_OK) {
         std::fprintf(stderr, "GPUassert: %s %s %d\n",
@@ -603,6 +668,7 @@ void sort(int *in, int n) {
                      __FILE__, __LINE__);
         std::exit(st == LABSORT_ERR_HIP ? g_last_hip : 1);
     }
+    if (verify) verify_or_exit("order_array", in, (size_t)n, before);
 }
 
 }  // extern "C"

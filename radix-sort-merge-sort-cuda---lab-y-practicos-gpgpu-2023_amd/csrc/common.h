@@ -113,11 +113,6 @@ constexpr int MG_BLOCK = LABSORT_MG_BLOCK;  // r15 sweep: 512 x 8 keys (4096-key
 constexpr int MG_KPT = LABSORT_MG_KPT;
 constexpr int MG_TILE = MG_BLOCK * MG_KPT;
 constexpr int MG_MAX_TPB = 256;       // most consecutive output tiles per merge workgroup
-constexpr int MG_MAX_PAIRS = 4;       // explicit pairs of runs per merge level (up to 8 runs)
-struct MgPairs {
-    uint32_t np;  // 0: uniform runs
-    uint32_t pb[MG_MAX_PAIRS + 1], pm[MG_MAX_PAIRS], tpre[MG_MAX_PAIRS + 1];
-};
 #ifndef LABSORT_MG_BRACKET
 #define LABSORT_MG_BRACKET 8
 #endif
@@ -223,6 +218,14 @@ hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size
                            size_t d1, uint32_t flip, uint32_t *part, hipStream_t s);
 hipError_t launch_upper_bound(const uint32_t *keys, size_t n, uint32_t flip, const uint32_t *values, size_t nv,
                               uint32_t *out, hipStream_t s);
+// LABSORT_VERIFY=1 checks of the host-pointer drop-ins (api.hip)
+struct KeyPrint {
+    uint64_t s1, s2, x;  // sum, sum of squares, xor of a mixed hash (mod 2^64)
+};
+bool verify_enabled();
+KeyPrint key_print(const int *a, size_t n);
+void verify_or_exit(const char *who, const int *a, size_t n, const KeyPrint &before);
+
 hipError_t launch_count_descents(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *count, hipStream_t s);
 
 }  // namespace labsort

@@ -34,7 +34,9 @@ stages device tensors through host memory for a CPU backend in tests).
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import time
 
 import torch
 import torch.distributed as dist
@@ -73,6 +75,10 @@ class Ops:
     def key_le(self, x: int, y: int) -> bool:
         raise NotImplementedError
 
+    def argsort(self, t: torch.Tensor) -> torch.Tensor:
+        """Stable argsort of int32-stored keys in key order (int64 indices)."""
+        return torch.argsort(self.order(t), stable=True)
+
     def upper_bound(self, a: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
         """int64 tensor: number of keys of sorted `a` <= each value (key order)"""
         raise NotImplementedError
@@ -106,7 +112,22 @@ class HipOps(Ops):
         ws = self._workspace(t.numel())
         out = torch.empty_like(t) if out_of_place else t
         self.ls.sort_device(t, out, t.numel(), key=self.key, algo=self.algo, workspace=ws, stream=self.stream)
+        # the kernels' own error report (a look-back spin that expired); synchronises
+        self.ls.workspace_status(ws, t.numel(), self.algo, stream=self.stream)
         return out
+
+    def argsort(self, t):
+        """Stable argsort by the labsort key/value sort of (key, index) pairs."""
+        n = t.numel()
+        if n == 0:
+            return torch.zeros(0, dtype=torch.int64, device=t.device)
+        idx = torch.arange(n, dtype=torch.int32, device=t.device)
+        ko, vo = torch.empty_like(t), torch.empty_like(idx)
+        ws = torch.empty(max(self.ls.pairs_workspace_bytes(n, "auto"), 256), dtype=torch.uint8, device=t.device)
+        self.ls.sort_pairs_device(t.contiguous(), idx, ko, vo, n, key=self.key, algo="auto", workspace=ws,
+                                  stream=self.stream)
+        self.ls.pairs_workspace_status(ws, n, "auto", stream=self.stream)
+        return vo.to(torch.int64)
 
     def merge(self, a, b, d0, d1):
         out = torch.empty(max(d1 - d0, 1), dtype=torch.int32, device=a.device if a.numel() else b.device)
@@ -152,16 +173,32 @@ class P2PComm:
 
     def __init__(self, group=None):
         self.group = group
+        self.sent_bytes = 0   # key bytes this rank sent over point-to-point ops
+        self.p2p_rounds = 0   # exchange calls (one partner, or all peers at once)
+        self.timed = False    # bench: synchronise around each exchange and add its wall time
+        self.exchange_s = 0.0
+
+    def _sync(self):
+        if self.timed and torch.cuda.is_available():
+            torch.cuda.synchronize()
 
     def exchange(self, send: torch.Tensor, recv: torch.Tensor, partner: int) -> None:
+        self.sent_bytes += send.numel() * send.element_size()
+        self.p2p_rounds += 1
+        self._sync()
+        t0 = time.perf_counter()
         g = self.group
         ops = [dist.P2POp(dist.isend, send, partner, group=g), dist.P2POp(dist.irecv, recv, partner, group=g)]
         for r in dist.batch_isend_irecv(ops):
             r.wait()
+        self._sync()
+        self.exchange_s += time.perf_counter() - t0
 
     def exchange_all(self, sends: list, recvs: list, rank: int) -> None:
         """sends[j] -> rank j, recvs[j] <- rank j for every peer j != rank, all posted
         together (one group: every xGMI link busy at once); empty pieces are skipped."""
+        self.sent_bytes += sum(x.numel() * x.element_size() for j, x in enumerate(sends) if j != rank)
+        self.p2p_rounds += 1
         g = self.group
         ops = []
         for j in range(len(sends)):
@@ -171,9 +208,13 @@ class P2PComm:
                 ops.append(dist.P2POp(dist.isend, sends[j], j, group=g))
             if recvs[j].numel():
                 ops.append(dist.P2POp(dist.irecv, recvs[j], j, group=g))
+        self._sync()
+        t0 = time.perf_counter()
         if ops:
             for r in dist.batch_isend_irecv(ops):
                 r.wait()
+        self._sync()
+        self.exchange_s += time.perf_counter() - t0
 
     def all_gather(self, t: torch.Tensor) -> list:
         out = [torch.empty_like(t) for _ in range(dist.get_world_size(self.group))]
@@ -233,13 +274,10 @@ def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, str
     other = torch.empty_like(samp)
     comm.exchange(samp.contiguous(), other, partner)
     Ls, Hs = (samp, other) if keep_low else (other, samp)
-    Lh, Hh = Ls.cpu().tolist(), Hs.cpu().tolist()
-    # first sample j with P(j*stride) false
-    j = 0
-    while j < len(Lh) and ops.key_le(Lh[j], Hh[j]):
-        j += 1
+    # first sample j with P(j*stride) false (vectorised on the device, one host read)
+    j = _first_false(ops.order(Ls) <= ops.order(Hs))
     lo = 0 if j == 0 else (j - 1) * stride + 1  # P(lo-1) true (or lo = 0)
-    hi = m if j == len(Lh) else j * stride      # P(hi) false (or hi = m)
+    hi = m if j == Ls.numel() else j * stride   # P(hi) false (or hi = m)
     # window: L[lo:hi] and H[m-1-(hi-1) : m-1-lo+1] = H[m-hi : m-lo]
     if hi > lo:
         if keep_low:
@@ -249,14 +287,25 @@ def _split_count(ops: Ops, mine: torch.Tensor, partner: int, keep_low: bool, str
         owin = torch.empty_like(win)
         comm.exchange(win, owin, partner)
         Lw, Hw = (win, owin) if keep_low else (owin, win)
-        Lw, Hw = Lw.cpu().tolist(), Hw.cpu().tolist()
-        # P(i) = L[i] <= H[m-1-i], i in [lo, hi): L[i] = Lw[i-lo], H[m-1-i] = Hw[(m-1-i)-(m-hi)] = Hw[hi-1-i]
-        c = lo
-        while c < hi and ops.key_le(Lw[c - lo], Hw[hi - 1 - c]):
-            c += 1
+        # P(i) = L[i] <= H[m-1-i], i in [lo, hi): L[i] = Lw[i-lo], H[m-1-i] = Hw[hi-1-i]
+        c = lo + _first_false(ops.order(Lw) <= ops.order(Hw.flip(0)))
     else:
         c = lo
     return m - c
+
+
+def _first_false(p: torch.Tensor) -> int:
+    """Index of the first False of a true-then-false predicate vector (len if none)."""
+    if p.numel() == 0:
+        return 0
+    return int((~p).to(torch.int32).argmax().item()) if not bool(p.all()) else p.numel()
+
+
+def _on_stream(ops):
+    """Run the schedule's torch work on the stream the local operations use, so a
+    caller that passes HipOps(stream=s) without entering it gets ordered work."""
+    s = getattr(ops, "stream", None)
+    return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
 
 
 def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, stride: int = 4096,
@@ -264,6 +313,11 @@ def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, s
     """Sort the global array whose rank-r shard is `local` (equal shard sizes).
     Returns this rank's shard of the sorted array (global ranks r*m .. r*m+m-1).
     `local` is sorted in place unless copy_input (then it is left untouched)."""
+    with _on_stream(ops):
+        return _dist_sort(local, ops, group, partial, stride, copy_input, comm)
+
+
+def _dist_sort(local, ops, group, partial, stride, copy_input, comm):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     comm = comm if comm is not None else P2PComm(group)
@@ -298,7 +352,16 @@ def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, s
 def dist_sort_splitters(local: torch.Tensor, ops: Ops, group=None, comm=None, copy_input: bool = False,
                         oversample: int = 1024) -> torch.Tensor:
     """Sort the global array whose rank-r shard is `local` with one all-peer exchange.
-    Returns this rank's contiguous range of the sorted array (ranges in rank order)."""
+    Returns this rank's contiguous range of the sorted array (ranges in rank order).
+
+    Splitters are (key, source rank, position) triples, so runs of one repeated key
+    are cut between ranks like any other keys: every range stays within the sample
+    granularity (about n/oversample keys) of its share, even for constant input."""
+    with _on_stream(ops):
+        return _dist_sort_splitters(local, ops, group, comm, copy_input, oversample)
+
+
+def _dist_sort_splitters(local, ops, group, comm, copy_input, oversample):
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     comm = comm if comm is not None else P2PComm(group)
@@ -306,20 +369,36 @@ def dist_sort_splitters(local: torch.Tensor, ops: Ops, group=None, comm=None, co
     if world == 1:
         return a
     m = a.numel()
-    # regular sample of every sorted shard -> common splitters at the p-1 quantiles
-    s = oversample * world  # same sample size on every rank (all_gather), repeats if m < s
+    # regular sample of every sorted shard: (key, position); the same sample size on
+    # every rank (all_gather), positions repeat if m < s
+    s = oversample * world
     idx = (torch.arange(s, device=a.device, dtype=torch.int64) * m) // s
     samp = a[idx].contiguous() if m else torch.zeros(s, dtype=a.dtype, device=a.device)
-    valid = torch.tensor([1 if m else 0], dtype=torch.int32, device=a.device)
+    meta = torch.cat([idx, torch.tensor([1 if m else 0], dtype=torch.int64, device=a.device)])
     samples = comm.all_gather(samp)
-    valids = torch.cat(comm.all_gather(valid)).cpu().tolist()  # ranks with an empty shard sample nothing
-    pool = torch.cat([x for x, v in zip(samples, valids) if v]) if any(valids) else samp
-    order = ops.order(pool)
-    srt = pool[torch.argsort(order, stable=True)]
-    q = (torch.arange(1, world, device=a.device, dtype=torch.int64) * srt.numel()) // world
-    splitters = srt[q].contiguous()
-    # cut points: piece j = keys in (splitter[j-1], splitter[j]]
-    cuts = ops.upper_bound(a, splitters) if m else torch.zeros(world - 1, dtype=torch.int64, device=a.device)
+    metas = comm.all_gather(meta)
+    valid = [int(x) for x in torch.stack([mt[-1] for mt in metas]).cpu().tolist()]  # empty shards sample nothing
+    ranks_ok = [r for r in range(world) if valid[r]]
+    if not ranks_ok:
+        ranks_ok = [rank]
+    pool = torch.cat([samples[r] for r in ranks_ok])
+    pool_rank = torch.cat([torch.full((s,), r, dtype=torch.int64, device=a.device) for r in ranks_ok])
+    pool_pos = torch.cat([metas[r][:-1] for r in ranks_ok])
+    # rank order + ascending positions per rank + a stable sort by key = (key, rank, pos) order
+    srt = ops.argsort(pool)
+    q = srt[(torch.arange(1, world, device=a.device, dtype=torch.int64) * pool.numel()) // world]
+    spl_key, spl_rank, spl_pos = pool[q].contiguous(), pool_rank[q], pool_pos[q]
+    # cut j on this rank: keys before splitter j in (key, rank, pos) order
+    if m:
+        f = 0x80000000 if getattr(ops, "key", "u32") == "i32" else 0
+        o = ops.order(spl_key)
+        prev = ((o - 1).clamp(min=0) ^ f) & 0xFFFFFFFF            # key just below, in key order
+        prev = torch.where(prev >= 2**31, prev - 2**32, prev).to(torch.int32)
+        both = ops.upper_bound(a, torch.cat([spl_key, prev]))
+        ub, lb = both[:world - 1], torch.where(o == 0, torch.zeros_like(o), both[world - 1:])
+        cuts = torch.where(spl_rank > rank, ub, torch.where(spl_rank < rank, lb, spl_pos + 1))
+    else:
+        cuts = torch.zeros(world - 1, dtype=torch.int64, device=a.device)
     bounds = [0] + [int(c) for c in cuts.cpu().tolist()] + [m]
     sizes = torch.tensor([bounds[j + 1] - bounds[j] for j in range(world)], dtype=torch.int64, device=a.device)
     all_sizes = torch.stack(comm.all_gather(sizes)).cpu()  # all_sizes[i][j] = rank i -> rank j

@@ -40,6 +40,7 @@ BIG = [  # (name, log2n, seed, dist)
     ("2^24_u32", 24, 0x5EED0004, "u32"),
     ("2^24_mod1000", 24, 0x5EED0004, "mod1000"),
     ("config3_2^28_u32", 28, 0x5EED0003, "u32"),
+    ("config5_2^30_u32", 30, 0x5EED0005, "u32"),
 ]
 
 
@@ -49,6 +50,8 @@ def sha(a: np.ndarray) -> str:
 
 def main():
     O.build()
+    if len(sys.argv) > 2 and sys.argv[1] == "--big":
+        return add_big(sys.argv[2:])
     small = {}
     for di, dist in enumerate(SMALL_DISTS):
         for n in SMALL_N:
@@ -82,8 +85,16 @@ def main():
     else:
         raise SystemExit("no F5 counter-example found")
 
-    big = {}
+    add_big([name for name, *_ in BIG], fresh=True)
+
+
+def add_big(names, fresh=False):
+    """(Re)compute the big.json entries `names` (python make_golden.py --big NAME...)."""
+    path = os.path.join(HERE, "big.json")
+    big = {} if fresh else json.load(open(path))
     for name, lg, seed, dist in BIG:
+        if name not in names:
+            continue
         a = O.gen(1 << lg, seed, dist)
         b = a.copy()
         O.lib().oracle_par_sort_u32(b.ctypes.data, b.size, os.cpu_count() or 1)
@@ -96,7 +107,7 @@ def main():
             big[name]["sha256_sorted_i32"] = sha(c)
         print(name, big[name]["sha256_sorted_u32"][:16])
         del a, b
-    with open(os.path.join(HERE, "big.json"), "w") as f:
+    with open(path, "w") as f:
         json.dump(big, f, indent=1)
 
 

@@ -92,6 +92,9 @@ def run(world, cfg):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if cfg.get("max_share"):
+        sizes = [res[r].size for r in range(world)]
+        assert max(sizes) <= cfg["max_share"] * cfg["m"], sizes
     return np.concatenate([res[r] for r in range(world)])
 
 
@@ -107,6 +110,10 @@ CFGS = [
     dict(m=3001, dist="u32", seed=0x5EED000A, key="i32", exchange="splitters", oversample=3),
     dict(m=100, dist="const", seed=3, key="u32", exchange="splitters"),
     dict(m=1, dist="u32", seed=4, key="u32", exchange="splitters"),
+    # repeated keys are cut between ranks by (key, rank, position) splitters: every
+    # range stays near its share (a constant input used to land on one rank)
+    dict(m=4000, dist="const", seed=5, key="u32", exchange="splitters", max_share=1.05),
+    dict(m=4000, dist="mod100", seed=6, key="i32", exchange="splitters", max_share=1.05),
 ]
 
 
@@ -121,6 +128,12 @@ def test_dist_sort_gloo(oracle, world, ci):
                                for r in range(world)])
     exp = oracle.sort_i32(full.view(np.int32)).view(np.uint32) if cfg["key"] == "i32" else oracle.sort_u32(full)
     np.testing.assert_array_equal(got.view(np.uint32), exp)
+
+
+@pytest.mark.parametrize("ci", [0, 6, 11, 12])
+def test_dist_sort_gloo_world8(oracle, ci):
+    """BASELINE config 5's rank count (8) on CPU: bitonic network and splitter exchange."""
+    test_dist_sort_gloo(oracle, 8, ci)
 
 
 def test_schedule_shape():

@@ -39,7 +39,7 @@ def _worker(rank, world, port, cfg, q):
         m = cfg["m"]
         t = torch.empty(m, dtype=torch.int32, device="cuda")
         ls.fill(t, m, cfg["seed"], cfg["dist"], first=rank * m)
-        ops = D.HipOps(ls, key=cfg["key"], local_algo=cfg["algo"], kway=cfg.get("kway", False))
+        ops = D.HipOps(ls, key=cfg["key"], local_algo=cfg["algo"], kway=cfg.get("kway", True))
         if cfg.get("exchange") == "splitters":
             out = D.dist_sort_splitters(t, ops, copy_input=True, comm=D.HostStagedComm())
         else:
@@ -62,6 +62,9 @@ def run(world, cfg):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if cfg.get("max_share"):
+        sizes = [res[r].size for r in range(world)]
+        assert max(sizes) <= cfg["max_share"] * cfg["m"], sizes
     return np.concatenate([res[r] for r in range(world)])
 
 
@@ -70,12 +73,17 @@ CFGS = [
     dict(m=1 << 20, dist="u32", seed=0x5EED0005, key="u32", algo="radix", partial=True, stride=4096),
     dict(m=65_537, dist="mod100", seed=0x5EED0006, key="u32", algo="merge", partial=True, stride=1000),
     dict(m=50_000, dist="u32", seed=0x5EED0007, key="i32", algo="radix", partial=False, stride=64),
+    # splitter exchange; received runs merged by the product default (one K-way
+    # labsort_merge_runs pass), and one config through the labsort_merge tree
     dict(m=1 << 20, dist="u32", seed=0x5EED0008, key="u32", algo="radix", exchange="splitters"),
     dict(m=300_001, dist="mod1000", seed=0x5EED0009, key="i32", algo="radix", exchange="splitters"),
-    dict(m=70_000, dist="const", seed=0x5EED000A, key="u32", algo="radix", exchange="splitters"),
-    # received runs merged in one K-way pass (labsort_merge_runs)
-    dict(m=1 << 20, dist="u32", seed=0x5EED000B, key="u32", algo="radix", exchange="splitters", kway=True),
-    dict(m=200_003, dist="mod100", seed=0x5EED000C, key="i32", algo="radix", exchange="splitters", kway=True),
+    dict(m=70_000, dist="const", seed=0x5EED000A, key="u32", algo="radix", exchange="splitters", max_share=1.02),
+    dict(m=1 << 20, dist="u32", seed=0x5EED000B, key="u32", algo="radix", exchange="splitters", kway=False),
+    dict(m=200_003, dist="mod100", seed=0x5EED000C, key="i32", algo="radix", exchange="splitters",
+         max_share=1.02),
+    dict(m=150_000, dist="sorted", seed=0x5EED000D, key="u32", algo="radix", exchange="splitters",
+         max_share=1.02),
+    dict(m=1, dist="u32", seed=0x5EED000E, key="u32", algo="radix", exchange="splitters"),  # tiny shards
 ]
 
 
@@ -87,3 +95,10 @@ def test_dist_sort_hip(oracle, world, ci):
     full = oracle.gen(cfg["m"] * world, cfg["seed"], cfg["dist"])
     exp = oracle.sort_i32(full.view(np.int32)).view(np.uint32) if cfg["key"] == "i32" else oracle.sort_u32(full)
     np.testing.assert_array_equal(got, exp)
+
+
+@pytest.mark.parametrize("ci", [1, 4, 6, 7, 8])
+def test_dist_sort_hip_world8(oracle, ci):
+    """BASELINE config 5's rank count: 8 ranks (sharing cuda:0, host-staged exchange)
+    through the HIP local sorts and merges, bitonic network and splitter exchange."""
+    test_dist_sort_hip(oracle, 8, ci)

@@ -39,6 +39,38 @@ def test_fullsize_sha(ls, torch_gpu, name, algo):
     assert sha(got) == c["sha256_sorted_u32"]
 
 
+@pytest.mark.parametrize("name", ["config2_2^20_u32", "2^24_u32", "2^24_mod1000"])
+@pytest.mark.parametrize("algo", ["radix", "merge"])
+def test_fullsize_sha_i32(ls, torch_gpu, name, algo):
+    """The same inputs in int32 order (sign-flipped digits and comparisons)."""
+    torch = torch_gpu
+    c = BIG[name]
+    n = 1 << c["log2n"]
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, c["seed"], c["dist"])
+    ls.sort_device(t, t, n, key="i32", algo=algo)
+    torch.cuda.synchronize()
+    assert sha(t.cpu().numpy()) == c["sha256_sorted_i32"]
+
+
+def test_fullsize_2e30_merge(ls, torch_gpu):
+    """BASELINE config 5's whole array (2^30 uint32 keys, 4 GiB) merge-sorted on one
+    MI355X: the single-GPU counterpart of the 8-GPU run, checked word for word."""
+    torch = torch_gpu
+    c = BIG["config5_2^30_u32"]
+    n = 1 << c["log2n"]
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, c["seed"], c["dist"])
+    ws = torch.empty(ls.workspace_bytes(n, "merge"), dtype=torch.uint8, device="cuda")
+    ls.sort_device(t, t, n, algo="merge", workspace=ws)
+    torch.cuda.synchronize()
+    del ws
+    got = t.cpu().numpy().view(np.uint32)
+    del t
+    assert int(got[0]) == c["first"] and int(got[-1]) == c["last"] and int(got[n // 2]) == c["median"]
+    assert sha(got) == c["sha256_sorted_u32"]
+
+
 def test_fullsize_inplace_repeat(ls, torch_gpu):
     """Same 2^28 input sorted 3 times in place and out of place: identical results
     (the look-back protocol is deterministic whatever the tile timing)."""

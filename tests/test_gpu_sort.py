@@ -341,12 +341,56 @@ def test_sort_device_pass_structure(ls, oracle, torch_gpu, mask, name, key, n):
     np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key), err_msg=name)
 
 
-@pytest.mark.parametrize("n", [1, 100, 8191, 8193, 16 * 8192 - 1, 16 * 8192 + 1, 3 * 16 * 8192 + 4097])
+OSP_TILE = 16384   # k_onesweep_p tile (csrc/common.h OSP_TILE)
+NSEG = 16         # position segments of the first pass (common.h NSEG)
+
+
+def _boundary_sizes():
+    ts = 32768    # labsort_tile_keys(): sizes up to it take the LDS tile-sort path
+    return sorted({1, 100, ts - 1, ts, ts + 1, ts + 100, 2 * OSP_TILE + 1, NSEG * OSP_TILE - 1,
+                   NSEG * OSP_TILE, NSEG * OSP_TILE + 1, 3 * NSEG * OSP_TILE + OSP_TILE // 2 + 1})
+
+
+@pytest.mark.parametrize("n", _boundary_sizes())
 def test_sort_device_segment_boundaries(ls, oracle, torch_gpu, n):
-    """Sizes around the 16 position segments x 8192-key tiles of the first pass."""
+    """Sizes around the 16 position segments x 16384-key tiles of the first onesweep
+    pass, and just above the tile-sort small path (the smallest multi-tile look-back
+    chains)."""
     torch = torch_gpu
+    assert ls.tile_keys() == 32768
     a = oracle.gen(n, SEED + 17 + n, "u32")
     t = to_dev(torch, a)
     ls.sort_device(t, t, n, algo="radix")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(from_dev(t), oracle.sort_u32(a))
+
+
+@pytest.mark.parametrize("pairs", [False, True])
+def test_workspace_status_reports_device_error(ls, oracle, torch_gpu, pairs):
+    """A radix sort that a kernel flagged (look-back spin limit) is reported as
+    LABSORT_ERR_DEVICE by labsort_workspace_status, never as OK; the next sort on the
+    workspace clears the word.  The error word is the workspace's first word."""
+    torch = torch_gpu
+    n = 1 << 20
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, SEED + 40, "u32")
+    o = torch.empty_like(t)
+    if pairs:
+        v, vo = torch.arange(n, dtype=torch.int32, device="cuda"), torch.empty_like(t)
+        ws = torch.empty(ls.pairs_workspace_bytes(n, "radix"), dtype=torch.uint8, device="cuda")
+        run = lambda: ls.sort_pairs_device(t, v, o, vo, n, algo="radix", workspace=ws)  # noqa: E731
+        status = lambda: ls.pairs_workspace_status(ws, n, "radix")  # noqa: E731
+    else:
+        ws = torch.empty(ls.workspace_bytes(n, "radix"), dtype=torch.uint8, device="cuda")
+        run = lambda: ls.sort_device(t, o, n, algo="radix", workspace=ws)  # noqa: E731
+        status = lambda: ls.workspace_status(ws, n, "radix")  # noqa: E731
+    run()
+    status()  # clean sort: OK
+    ws[:4].view(torch.int32).fill_(1)  # what atomicOr(err, 1) leaves behind
+    with pytest.raises(ls.LabsortError, match="device-side"):
+        status()
+    # merge-path sorts have no error word: always OK
+    ls.workspace_status(ws, n, "merge")
+    run()
+    status()
+    np.testing.assert_array_equal(from_dev(o), oracle.sort_u32(oracle.gen(n, SEED + 40, "u32")))
