@@ -101,6 +101,35 @@ int labsort_workspace_status(const void *d_workspace, size_t n, int algo, void *
 /* The same for the last labsort_sort_pairs_device(n, algo) on d_workspace. */
 int labsort_pairs_workspace_status(const void *d_workspace, size_t n, int algo, void *stream);
 
+/* ---- one process, several GPUs (the reference is
+ * single-GPU, lab.cu:303-402) ----
+ * Sort a host buffer in place with nranks ranks: rank r takes the contiguous shard
+ * h_keys[r*n/p, (r+1)*n/p) over its own PCIe link (one host thread per rank), sorts it
+ * locally (LABSORT_ALGO_AUTO), then the ranks agree on p-1 (key, rank, position)
+ * splitters from a regular sample of every sorted shard, cut their shards at them
+ * (labsort_upper_bound), exchange piece j -> rank j, merge the p received runs in one
+ * K-way pass (labsort_merge_runs) and copy their ranges back to their global offsets.
+ * transport: LABSORT_XFER_RCCL (ncclSend/ncclRecv to every peer in one group; one rank
+ * per device), LABSORT_XFER_PEER (hipMemcpyPeerAsync; ranks may share a device) or
+ * LABSORT_XFER_AUTO (RCCL for distinct devices, peer copies otherwise).  Synchronous.
+ * order_array / sort use it when LABSORT_GPUS > 1. */
+#define LABSORT_XFER_AUTO 0
+#define LABSORT_XFER_RCCL 1
+#define LABSORT_XFER_PEER 2
+#define LABSORT_MULTI_MAX_RANKS 8
+/* phases of labsort_multi_timing, ms of the last call (max over ranks where per rank):
+ * 0 H2D, 1 local sort, 2 splitters + cut points, 3 exchange, 4 merge, 5 D2H, 6 total */
+#define LABSORT_MULTI_PHASES 7
+int labsort_sort_host_multi(void *h_keys, size_t n, int key_type, int ngpus);  /* devices 0..ngpus-1 */
+int labsort_sort_host_ranks(void *h_keys, size_t n, int key_type, int nranks, const int *devices, int transport);
+int labsort_multi_timing(double *phase_ms, int nphases, size_t *max_sent_bytes);
+int labsort_multi_last_hip_error(void);
+/* The exchange plan alone, on host shards (sorted h_shards[r][0..m[r]) per rank;
+ * std::upper_bound stands in for the device bound queries): writes the cut points,
+ * h_cuts[r*(nranks+1) + j] = first position of the piece rank r sends to rank j.
+ * Test hook for the schedule; no GPU involved. */
+int labsort_multi_plan(const uint32_t *const *h_shards, const size_t *m, int nranks, int key_type, size_t *h_cuts);
+
 /* ---- key/value (sort_by_key; no lab.cu counterpart, the reference sorts
  * keys only) ----
  * Stable sort of n (key, 4-byte payload) pairs: d_keys_in/d_vals_in -> d_keys_out/

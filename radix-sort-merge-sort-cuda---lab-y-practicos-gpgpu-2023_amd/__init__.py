@@ -42,7 +42,11 @@ C_SYMBOLS = [
     "labsort_merge_runs_workspace_bytes", "labsort_merge_runs",
     "labsort_pair_tile_keys", "labsort_pairs_workspace_bytes", "labsort_sort_pairs_device",
     "labsort_workspace_status", "labsort_pairs_workspace_status",
+    "labsort_sort_host_multi", "labsort_sort_host_ranks", "labsort_multi_timing", "labsort_multi_last_hip_error",
+    "labsort_multi_plan",
 ]
+XFER = {"auto": 0, "rccl": 1, "peer": 2}
+MULTI_PHASES = ["h2d", "local_sort", "plan", "exchange", "merge", "d2h", "total"]
 CXX_SYMBOLS = ["_Z11order_arrayPii", "_Z16order_with_trustPii"]
 
 
@@ -94,6 +98,10 @@ def _load() -> ctypes.CDLL:
     L.labsort_pairs_workspace_bytes.argtypes = [sz, i]
     L.labsort_sort_pairs_device.argtypes = [p, p, p, p, sz, i, i, p, sz, p]
     L.labsort_workspace_status.argtypes = [p, sz, i, p]
+    L.labsort_sort_host_multi.argtypes = [p, sz, i, i]
+    L.labsort_sort_host_ranks.argtypes = [p, sz, i, i, p, i]
+    L.labsort_multi_timing.argtypes = [ctypes.POINTER(ctypes.c_double), i, ctypes.POINTER(sz)]
+    L.labsort_multi_plan.argtypes = [ctypes.POINTER(p), ctypes.POINTER(sz), i, i, ctypes.POINTER(sz)]
     L.labsort_pairs_workspace_status.argtypes = [p, sz, i, p]
     L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
     L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
@@ -172,6 +180,52 @@ def order_with_trust(a: np.ndarray) -> None:
     """thrust::sort on the host pointer (lab.cu:404): rocThrust's sequential CPU sort."""
     assert a.dtype == np.int32 and a.flags["C_CONTIGUOUS"]
     getattr(lib, "_Z16order_with_trustPii")(a.ctypes.data, a.size)
+
+
+def _check_multi(status: int, what: str) -> None:
+    if status == ERR_HIP:
+        raise LabsortError(f"{what} failed: HIP runtime error: "
+                           + lib.labsort_hip_error_string(lib.labsort_multi_last_hip_error()).decode())
+    _check(status, what)
+
+
+def sort_host_multi(a: np.ndarray, ngpus: int) -> None:
+    """Sort a uint32/int32 numpy array in place across devices 0..ngpus-1 of this
+    process (labsort_sort_host_multi: per-GPU shards, RCCL splitter exchange)."""
+    key = "i32" if a.dtype == np.int32 else "u32"
+    assert a.dtype in (np.int32, np.uint32) and a.flags["C_CONTIGUOUS"]
+    _check_multi(lib.labsort_sort_host_multi(a.ctypes.data, a.size, KEY[key], ngpus), "sort_host_multi")
+
+
+def sort_host_ranks(a: np.ndarray, devices, transport: str = "auto") -> None:
+    """As sort_host_multi with an explicit rank -> device map (ranks may share a
+    device with transport "peer": the whole schedule on one GPU)."""
+    key = "i32" if a.dtype == np.int32 else "u32"
+    assert a.dtype in (np.int32, np.uint32) and a.flags["C_CONTIGUOUS"]
+    dv = (ctypes.c_int * len(devices))(*devices)
+    _check_multi(lib.labsort_sort_host_ranks(a.ctypes.data, a.size, KEY[key], len(devices), dv, XFER[transport]),
+                 "sort_host_ranks")
+
+
+def multi_timing() -> tuple[dict, int]:
+    """Phase times (ms) of the last multi-GPU host sort and the most key bytes one
+    rank sent to its peers."""
+    ms = (ctypes.c_double * len(MULTI_PHASES))()
+    sent = ctypes.c_size_t(0)
+    _check(lib.labsort_multi_timing(ms, len(MULTI_PHASES), ctypes.byref(sent)), "multi_timing")
+    return dict(zip(MULTI_PHASES, list(ms))), sent.value
+
+
+def multi_plan(shards, key: str = "u32") -> np.ndarray:
+    """Cut points of the multi-GPU exchange plan for sorted host shards (test hook):
+    cuts[r, j] = first position of the piece rank r sends to rank j (cuts[r, p] = m_r)."""
+    arrs = [np.ascontiguousarray(x).view(np.uint32) for x in shards]
+    p = len(arrs)
+    ptrs = (ctypes.c_void_p * p)(*[x.ctypes.data if x.size else None for x in arrs])
+    ms = (ctypes.c_size_t * p)(*[x.size for x in arrs])
+    cuts = (ctypes.c_size_t * (p * (p + 1)))()
+    _check(lib.labsort_multi_plan(ptrs, ms, p, KEY[key], cuts), "multi_plan")
+    return np.array(list(cuts), dtype=np.int64).reshape(p, p + 1)
 
 
 def _default_algo() -> int:

@@ -277,6 +277,13 @@ int default_algo() {
     return LABSORT_ALGO_AUTO;
 }
 
+// LABSORT_GPUS=p (p > 1): the host drop-ins sort across devices 0..p-1
+// (labsort_sort_host_multi); unset, 0 or 1: one GPU.
+int multi_gpus() {
+    const char *e = std::getenv("LABSORT_GPUS");
+    return e ? std::atoi(e) : 0;
+}
+
 // LABSORT_ALGO_AUTO -> the algorithm that runs.  Measured on MI355X (r15,
 // harness/exp/small_n.py, device-resident): merge 0.054 / 0.119 / 0.202 ms vs radix
 // 0.134 / 0.220 / 0.286 ms at 2^16 / 2^20 / 2^22; equal at 2^23; radix faster above.
@@ -539,7 +546,7 @@ int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint3
     uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
     uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
     Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
-    HIP_TRY(hipMemsetAsync(ws + L.off_hist, 0, L.zero_bytes, s));
+    HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes, s));
     {
         TimingScope ts(LABSORT_K_HISTOGRAM, s);
         HIP_TRY(launch_histogram(ki, n, flip, 8, hist, s));
@@ -661,12 +668,15 @@ void sort(int *in, int n) {
     const bool verify = verify_enabled();
     KeyPrint before{};
     if (verify) before = key_print(in, (size_t)n);
-    const int st = labsort_sort_host(in, (size_t)n, LABSORT_KEY_I32, default_algo());
+    const int gpus = multi_gpus();
+    const int st = gpus > 1 ? labsort_sort_host_multi(in, (size_t)n, LABSORT_KEY_I32, gpus)
+                            : labsort_sort_host(in, (size_t)n, LABSORT_KEY_I32, default_algo());
     if (st != LABSORT_OK) {
+        const int hip = gpus > 1 ? labsort_multi_last_hip_error() : g_last_hip;
         std::fprintf(stderr, "GPUassert: %s %s %d\n",
-                     st == LABSORT_ERR_HIP ? hipGetErrorString((hipError_t)g_last_hip) : labsort_error_string(st),
-                     __FILE__, __LINE__);
-        std::exit(st == LABSORT_ERR_HIP ? g_last_hip : 1);
+                     st == LABSORT_ERR_HIP ? hipGetErrorString((hipError_t)hip) : labsort_error_string(st), __FILE__,
+                     __LINE__);
+        std::exit(st == LABSORT_ERR_HIP && hip ? hip : 1);
     }
     if (verify) verify_or_exit("order_array", in, (size_t)n, before);
 }
