@@ -404,7 +404,7 @@ def main():
                   "8-bit LSD onesweep passes" if args.pair_algo == "radix" else "LDS tile sort + merge-path passes")
               }[args.algo]
         if world > 1:
-            how = ("splitter exchange (pairwise send/recv to all peers at once) + merge tree"
+            how = ("splitter exchange (pairwise send/recv to all peers at once) + one K-way merge of the received runs"
                    if args.exchange == "splitters" else "bitonic pairwise merge-split network")
             workload = (f"merge sort across {world} GPUs: local radix sort of 2^{args.log2n} uint32 keys per GPU "
                         f"+ {how} over RCCL/xGMI (BASELINE config 5 shape, weak scaling)")
