@@ -159,6 +159,77 @@ __global__ __launch_bounds__(1024) void k_abut_own(const uint32_t *a, uint32_t *
         }
     }
 }
+// runs of K consecutive tiles per workgroup (tiles dealt per XCD group as XL): the
+// onesweep shape where one workgroup scatters K consecutive tiles of a chain in turn.
+// CARRY: inside a workgroup's run of tiles, the granule a tile shares with the next
+// tile is written once, whole, by the next tile (the tail keys carried in LDS); only
+// the first tile's head and the last tile's tail granules are shared across workgroups.
+// VEC: tile keys loaded as uint4 per lane (4 consecutive keys) instead of 4-B lanes.
+template <int RUN, int K, int CARRY, int VEC = 0>
+__global__ __launch_bounds__(1024) void k_abut_run(const uint32_t *a, uint32_t *b, uint32_t ntiles) {
+    const uint32_t tid = threadIdx.x;
+    const size_t stride = (size_t)ntiles * RUN + 64;
+    const uint32_t g = blockIdx.x & 7u, per = ntiles / 8u, runs = per / K;
+    for (uint32_t q = blockIdx.x >> 3; q < runs; q += gridDim.x >> 3) {
+        for (uint32_t kk = 0; kk < (uint32_t)K; ++kk) {
+            const uint32_t t = g * per + q * K + kk;
+            uint32_t k[16];
+            if (VEC) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(a + (size_t)t * 16384);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint4 v = src[j * 1024 + tid];
+                    k[4 * j] = v.x; k[4 * j + 1] = v.y; k[4 * j + 2] = v.z; k[4 * j + 3] = v.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) k[j] = a[(size_t)t * 16384 + j * 1024 + tid];
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t i = j * 1024 + tid, d = i / RUN, u = i % RUN;
+                const uint32_t sh = (d * 5u + 3u) & 31u;
+                const size_t rs = d * stride + sh + (size_t)t * RUN, re = rs + RUN, pos = rs + u;
+                if (CARRY) {
+                    const size_t hi = kk + 1 < (uint32_t)K ? (re & ~(size_t)15) : re;
+                    if (kk > 0 && u < (rs & 15)) b[(rs & ~(size_t)15) + u] = k[j];  // the carried head words
+                    if (pos < hi) b[pos] = k[j];
+                } else {
+                    b[pos] = k[j];
+                }
+            }
+        }
+    }
+}
+// gather: the reverse shape -- output tile T is written contiguously (whole lines) and
+// its keys are read as runs of RUN words from the locally sorted source tiles: logical
+// position L = T*16384 + i lies in bucket d = L / (ntiles*RUN), run t (source tile t),
+// word u; the run starts at a misaligned word offset inside source tile t
+template <int RUN, int XL, int VEC = 0>
+__global__ __launch_bounds__(1024) void k_gather(const uint32_t *a, uint32_t *b, uint32_t ntiles) {
+    const uint32_t tid = threadIdx.x;
+    const size_t bucket = (size_t)ntiles * RUN, tstride = 16384 + 32;
+    const uint32_t g = blockIdx.x & 7u, per = ntiles / 8u;
+    for (uint32_t q = XL ? blockIdx.x >> 3 : blockIdx.x; q < (XL ? per : ntiles); q += XL ? gridDim.x >> 3 : gridDim.x) {
+        const uint32_t T = XL ? g * per + q : q;
+        uint32_t k[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const size_t L = (size_t)T * 16384 + (VEC ? (j >> 2) * 4096 + tid * 4 + (j & 3) : j * 1024 + tid);
+            const size_t d = L / bucket, r = L % bucket, t = r / RUN, u = r % RUN;
+            const uint32_t sh = (uint32_t)((t * 37u + d * 11u) & 31u);
+            k[j] = a[t * tstride + d * RUN + sh + u];
+        }
+        if (VEC) {
+            uint4 *dst = reinterpret_cast<uint4 *>(b + (size_t)T * 16384);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dst[j * 1024 + tid] = make_uint4(k[4 * j], k[4 * j + 1], k[4 * j + 2], k[4 * j + 3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) b[(size_t)T * 16384 + j * 1024 + tid] = k[j];
+        }
+    }
+}
 // MODE 0: aligned runs of 64; 1: runs shifted by a per-(t,d) offset (region stride has
 // 64 words of slack per tile); 2: variable run lengths (lens[t*256+d], prefix offs).
 template <int MODE>
@@ -333,6 +404,48 @@ int main() {
     printf("abut-16xl  %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { k_abut<8, 1, 1><<<256, 1024>>>(in, out, ntiles); });
     printf("abut-8xl   %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 1, 0><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K1     %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 4, 0><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K4     %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 4, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K4c    %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 8, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K8c    %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 16, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K16c   %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 8, 0><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K8     %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 1, 0, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K1v    %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 8, 1, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K8cv   %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    t = timeit([&] { k_abut_run<64, 16, 1, 1><<<256, 1024>>>(in, out, ntiles); });
+    printf("run-64 K16cv  %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    {
+        uint32_t *src2;
+        CK(hipMalloc(&src2, (size_t)ntiles * (16384 + 32) * 4 + 4096));
+        CK(hipMemset(src2, 1, (size_t)ntiles * (16384 + 32) * 4));
+        t = timeit([&] { k_gather<64, 0><<<256, 1024>>>(src2, out, ntiles); });
+        printf("gather-64     %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        t = timeit([&] { k_gather<64, 1><<<256, 1024>>>(src2, out, ntiles); });
+        printf("gather-64xl   %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        t = timeit([&] { k_gather<64, 0, 1><<<256, 1024>>>(src2, out, ntiles); });
+        printf("gather-64v    %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        t = timeit([&] { k_gather<64, 0><<<512, 1024>>>(src2, out, ntiles); });
+        printf("gather-64 g512 %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        t = timeit([&] { k_gather<32, 0><<<256, 1024>>>(src2, out, ntiles); });
+        printf("gather-32     %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        t = timeit([&] { k_gather<32, 1><<<256, 1024>>>(src2, out, ntiles); });
+        printf("gather-32xl   %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        t = timeit([&] { k_gather<16, 1><<<256, 1024>>>(src2, out, ntiles); });
+        printf("gather-16xl   %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        t = timeit([&] { k_gather<8, 1><<<256, 1024>>>(src2, out, ntiles); });
+        printf("gather-8xl    %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        t = timeit([&] { k_gather<8, 1><<<512, 1024>>>(src2, out, ntiles); });
+        printf("gather-8xl g512 %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+        CK(hipFree(src2));
+    }
     CK(hipDeviceSynchronize());
     return 0;
 }

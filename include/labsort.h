@@ -41,13 +41,15 @@ extern "C" {
 #define LABSORT_ERR_DEVICE 3     /* a kernel reported an internal error (bounded spin expired) */
 
 /* algorithms */
-#define LABSORT_ALGO_RADIX 0     /* LSD radix, 8-bit digits, onesweep passes (default) */
+#define LABSORT_ALGO_RADIX 0     /* LSD radix, 8-bit digits: gathered passes for 2^16 <= n < 2^26,
+                                    onesweep scatter passes outside (LABSORT_RADIX_IMPL=onesweep or
+                                    =gather forces one) */
 #define LABSORT_ALGO_MERGE 1     /* LDS tile radix + merge-path merge passes */
 #define LABSORT_ALGO_RADIX1 2    /* LSD radix with 1-bit digits: letra.pdf's split, 32 passes */
 #define LABSORT_ALGO_AUTO 3      /* MERGE for n <= LABSORT_AUTO_MERGE_MAX_KEYS (fewer launches and
                                     less fixed cost at small n), RADIX above; the default of the
                                     host drop-ins order_array / sort (LABSORT_ALGO env overrides) */
-#define LABSORT_AUTO_MERGE_MAX_KEYS (1u << 22)
+#define LABSORT_AUTO_MERGE_MAX_KEYS (1u << 20)
 
 /* key types: how the 32-bit words are ordered */
 #define LABSORT_KEY_U32 0
@@ -69,7 +71,9 @@ extern "C" {
 #define LABSORT_K_TILE_SORT 2
 #define LABSORT_K_MERGE 3
 #define LABSORT_K_PARTITION 4
-#define LABSORT_K_COUNT 5
+#define LABSORT_K_GSWEEP 5       /* gathered radix pass (LABSORT_ALGO_RADIX, 2^16 <= n < 2^26) */
+#define LABSORT_K_GCOPY 6        /* its final gathered copy */
+#define LABSORT_K_COUNT 7
 
 /* ---- library info ---- */
 const char *labsort_version(void);

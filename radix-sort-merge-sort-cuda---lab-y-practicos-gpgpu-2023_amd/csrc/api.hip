@@ -143,6 +143,39 @@ MergeLayout merge_layout(size_t n) {
     return L;
 }
 
+// LABSORT_ALGO_RADIX from GS_MIN_N keys on: the gathered passes (gsweep.hip), unless
+// LABSORT_RADIX_IMPL=onesweep selects the scatter passes (kernels.hip k_onesweep_p)
+bool use_gather(size_t n) {
+    const char *e = std::getenv("LABSORT_RADIX_IMPL");
+    if (e && !std::strcmp(e, "gather")) return true;  // any n (experiments, tests)
+    if (n < GS_MIN_N || n >= GS_MAX_N) return false;
+    return !(e && !std::strcmp(e, "onesweep"));
+}
+
+// GsHooks callbacks: the same event pairs as TimingScope
+struct HookCtx {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+void hook_begin(void *ctx, int cls, hipStream_t s) {
+    (void)cls;
+    HookCtx *h = static_cast<HookCtx *>(ctx);
+    h->a = h->b = nullptr;
+    if (!g_timing_on) return;
+    if (hipEventCreate(&h->a) != hipSuccess || hipEventCreate(&h->b) != hipSuccess) {
+        h->a = h->b = nullptr;
+        return;
+    }
+    (void)hipEventRecord(h->a, s);
+}
+void hook_end(void *ctx, int cls, hipStream_t s) {
+    HookCtx *h = static_cast<HookCtx *>(ctx);
+    if (!h->a) return;
+    (void)hipEventRecord(h->b, s);
+    std::lock_guard<std::mutex> lk(g_timing_mu);
+    g_pending.push_back({cls, h->a, h->b});
+    h->a = h->b = nullptr;
+}
+
 bool small_path(size_t n, int algo) { return algo != LABSORT_ALGO_RADIX1 && n <= (size_t)TS_TILE; }
 
 int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int bits, char *ws, hipStream_t s) {
@@ -369,7 +402,11 @@ size_t labsort_workspace_bytes(size_t n, int algo) {
     algo = resolve_algo(algo, n);
     if (small_path(n, algo)) return 256;
     switch (algo) {
-    case LABSORT_ALGO_RADIX: return radix_layout(n, 8).total;
+    case LABSORT_ALGO_RADIX: {
+        const size_t r = radix_layout(n, 8).total;
+        const size_t g = gs_layout(n).total;
+        return r > g ? r : g;  // either implementation fits (LABSORT_RADIX_IMPL may change)
+    }
     case LABSORT_ALGO_RADIX1: return radix_layout(n, 1).total;
     case LABSORT_ALGO_MERGE: return merge_layout(n).total;
     default: return 0;
@@ -398,6 +435,11 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
     }
     char *ws = static_cast<char *>(d_ws);
     if (algo == LABSORT_ALGO_MERGE) return sort_merge(in, out, n, flip, ws, s);
+    if (algo == LABSORT_ALGO_RADIX && use_gather(n)) {
+        HookCtx hc;
+        HIP_TRY(launch_gsweep_sort(in, out, n, flip, ws, s, GsHooks{&hc, hook_begin, hook_end}));
+        return LABSORT_OK;
+    }
     return sort_radix(in, out, n, flip, algo == LABSORT_ALGO_RADIX1 ? 1 : 8, ws, s);
 }
 

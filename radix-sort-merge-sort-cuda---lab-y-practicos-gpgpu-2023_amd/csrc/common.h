@@ -162,6 +162,32 @@ struct KmRuns {
 hipError_t launch_kmerge(const uint32_t *in, uint32_t *out, KmRuns rs, uint32_t flip, uint32_t *ws, hipStream_t s);
 size_t km_workspace_words(size_t n);
 
+// ---- gathered LSD radix (gsweep.hip): tiles gathered run by run, sorted in LDS,
+// written contiguously; 8-bit digits, one tile per 512-thread workgroup, 3 per CU ----
+constexpr int GS_BLOCK = 512;
+#ifndef LABSORT_GS_KPT
+#define LABSORT_GS_KPT 16
+#endif
+constexpr int GS_KPT = LABSORT_GS_KPT;
+constexpr int GS_TILE = GS_BLOCK * GS_KPT;      // 8192 keys
+constexpr int GS_KMAX = 1024;                   // runs per tile listed in LDS (else per-lane search)
+constexpr int GS_GROUP = 64;                    // tiles per scan workgroup
+constexpr size_t GS_MIN_N = (size_t)1 << 16;    // LABSORT_ALGO_RADIX uses it for GS_MIN_N <= n < GS_MAX_N
+constexpr size_t GS_MAX_N = (size_t)1 << 26;    // (onesweep outside; measured crossovers)
+struct GsLayout {
+    size_t off_state, off_a, off_b, off_rt, off_mm, off_gsum, off_gsx, off_gx, off_gmm, off_ls[2], off_sr[2],
+        off_first[2], total;
+};
+GsLayout gs_layout(size_t n);
+// timing hooks around the pass and final-copy launches (api.hip's event scopes)
+struct GsHooks {
+    void *ctx;
+    void (*begin)(void *ctx, int kernel_class, hipStream_t s);
+    void (*end)(void *ctx, int kernel_class, hipStream_t s);
+};
+hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s,
+                              const GsHooks &hooks);
+
 constexpr int MAX_PASSES = 32;
 constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_SKIP = 0xFFu;
 constexpr uint32_t NEXT_NONE = 0xFFFFFFFFu;

@@ -1,0 +1,540 @@
+// gsweep.hip -- LSD radix sort whose passes gather their reads and write whole tiles.
+//
+// The onesweep pass (kernels.hip, k_onesweep_p) reads its tile contiguously and
+// scatters it: every (tile, digit) run of ~64 keys lands at an arbitrary word offset,
+// so the 64-B granules at run edges are written partially by two tiles.  On MI355X
+// that write shape caps a pass at ~0.55 ms for 2^28 keys (harness/exp/bw_probe.hip:
+// abutting misaligned 64-word runs 0.55 ms, the same runs read instead of written
+// 0.44 ms, a tiled copy 0.39 ms).  Here every pass reverses the shape:
+//
+//   pass p (k_gsweep): tile T of the pass's LOGICAL input -- the keys in the order
+//     the previous pass defines -- is gathered run by run from the previous pass's
+//     output, sorted by digit p in LDS (stable wave rank, as the onesweep pass), and
+//     written back CONTIGUOUSLY at T's own position: whole lines, no partial granules.
+//     The tile's digit counts and local offsets go to a row of `rt`.
+//   scan (k_gsum, k_gtop, k_gout): from the rows, the logical start of every
+//     (tile, digit) run (global digit offset + counts of earlier tiles) in digit-major
+//     order, its source address, and for every next-pass tile the first run it covers.
+//     This is the global exclusive scan of letra.pdf's split (lab.cu's per-bit
+//     "totalFalses" generalised to 256 digits) done once per pass over counts only.
+//   final (k_gcopy): the logical order after the last pass is the sorted array; one
+//     gathered read + contiguous write produces it.
+//
+// Pass 0 reads the input contiguously and also records every tile's digit min/max, so
+// passes whose digit is the same for every key are skipped on the device (the
+// deterministic counterpart of the reference's "stop when sorted", lab.cu:61).
+// No decoupled look-back, no spin: tiles of a pass are independent.
+//
+// Logical input of pass p >= 1 (previous pass q wrote buffer X): run (t, d) = the keys
+// of digit d in tile t of X, at X[t*TILE + lo(t,d)], length h(t,d); runs in the order
+// (d, t) are the keys in order.  Tables per buffer, digit-major, e = d*ntp + t:
+//   ls[e]     logical start of run e (ls[256*ntp] = n)
+//   sr[e]     source address t*TILE + lo(t,d)
+//   first[T]  e of the run holding logical position T*TILE; first[ntp]: position n-1
+#include "../../include/labsort.h"
+#include "common.h"
+#include "devutil.h"
+
+namespace labsort {
+
+namespace {
+
+constexpr int GB = GS_BLOCK, GK = GS_KPT, GT = GS_TILE, GW = GS_BLOCK / WAVE;
+#ifndef LABSORT_GS_WPE
+#define LABSORT_GS_WPE (GS_KPT > 16 ? 2 : 3)
+#endif
+constexpr int GS_WAVES_PER_EU = LABSORT_GS_WPE;  // launch-bounds occupancy hint (workgroups per CU)
+static_assert(GT == GB * GK && GW * WAVE == GB, "tile shape");
+
+struct GsTables {
+    uint32_t *ls, *sr, *first;
+};
+
+// Workspace header (first 512 B; word 0 is the labsort error word, never set here)
+struct GsState {
+    uint32_t err;
+    uint32_t cur;       // buffer holding the current logical order: 0 input (plain), 1 A, 2 B
+    uint32_t dmin[4];   // per digit, min / max over all keys (flipped digit values), from pass 0
+    uint32_t dmax[4];
+};
+
+__device__ __forceinline__ bool gs_active(const GsState *st, int pass) {
+    return pass == 0 || st->dmin[pass] != st->dmax[pass];
+}
+
+// tiles dealt per XCD: blocks b, b+8, b+16, ... (one XCD) take consecutive tiles, so a
+// run's neighbouring reads meet in one L2 (bw_probe: gather 0.49 -> 0.44 ms)
+__device__ __forceinline__ uint32_t gs_tile(uint32_t b, uint32_t ntp) {
+    const uint32_t per = (ntp + 7u) >> 3;
+    return (b & 7u) * per + (b >> 3);
+}
+
+struct GsRuns {
+    uint32_t bits[GT / 32];     // run-start bitmap over the tile's positions
+    uint32_t wpre[GT / 32];     // exclusive prefix of the bitmap words' popcounts
+    int32_t delta[GS_KMAX];     // per nonempty run, in order: source address - logical position
+    uint32_t wsum[8];
+};
+
+// Keys of tile T (positions L0 + wid*GK*64 + j*64 + lane) of the logical order held in
+// `src` with tables tb; sentinel past nvalid.  Block-uniform control flow (barriers).
+// The run of position p = (number of nonempty runs starting at or before p) - 1, read
+// off a start bitmap with one popcount, so the 16 slots of a lane are independent and
+// their loads issue back to back.
+__device__ __forceinline__ void gs_gather(const uint32_t *__restrict__ src, const GsTables &tb, uint32_t T,
+                                          uint32_t L0, uint32_t nvalid, uint32_t sentinel, GsRuns &g,
+                                          uint32_t (&k)[GK], uint32_t tid, uint32_t lane, uint32_t wid) {
+    const uint32_t e0 = tb.first[T], e1 = tb.first[T + 1];
+    const uint32_t K = e1 - e0 + 1;  // runs of the tile, empty ones included
+    const uint32_t pw = wid * (GK * WAVE) + lane;
+    if (K <= (uint32_t)GS_KMAX) {
+        constexpr int RPT = GS_KMAX / GB;  // run entries per thread
+        uint32_t rel[RPT], sr[RPT];
+        bool ne[RPT];
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            const uint32_t i = tid + (uint32_t)r * GB;
+            ne[r] = false;
+            rel[r] = sr[r] = 0;
+            if (i < K) {
+                const uint32_t a = tb.ls[e0 + i], b = tb.ls[e0 + i + 1];  // e0 + K <= 256 * ntp (sentinel)
+                sr[r] = tb.sr[e0 + i] - a;  // delta (mod 2^32)
+                ne[r] = b > a && a < L0 + nvalid;  // the bracket's last run may start at the next tile
+                rel[r] = a > L0 ? a - L0 : 0u;
+            }
+        }
+        if (tid < (uint32_t)(GT / 32)) g.bits[tid] = 0u;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RPT; ++r)
+            if (ne[r]) atomicOr(&g.bits[rel[r] >> 5], 1u << (rel[r] & 31u));
+        __syncthreads();
+        const uint32_t pc = tid < (uint32_t)(GT / 32) ? (uint32_t)__popc(g.bits[tid]) : 0u;
+        const uint32_t ex = block_excl_scan<GB, GT / 32>(pc, g.wsum);
+        if (tid < (uint32_t)(GT / 32)) g.wpre[tid] = ex;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < RPT; ++r) {
+            if (ne[r]) {
+                const uint32_t w = rel[r] >> 5;
+                g.delta[g.wpre[w] + (uint32_t)__popc(g.bits[w] & ((1u << (rel[r] & 31u)) - 1u))] = (int32_t)sr[r];
+            }
+        }
+        __syncthreads();
+        uint32_t addr[GK];
+#pragma unroll
+        for (int j = 0; j < GK; ++j) {
+            const uint32_t p = pw + (uint32_t)j * WAVE;
+            const uint32_t w = p >> 5, b = p & 31u;
+            const uint32_t m = b == 31u ? 0xFFFFFFFFu : (2u << b) - 1u;
+            const uint32_t idx = g.wpre[w] + (uint32_t)__popc(g.bits[w] & m) - 1u;
+            addr[j] = L0 + p + (uint32_t)g.delta[idx < (uint32_t)GS_KMAX ? idx : 0u];
+        }
+        if (nvalid == (uint32_t)GT) {
+#pragma unroll
+            for (int j = 0; j < GK; ++j) k[j] = src[addr[j]];
+        } else {
+#pragma unroll
+            for (int j = 0; j < GK; ++j) k[j] = pw + (uint32_t)j * WAVE < nvalid ? src[addr[j]] : sentinel;
+        }
+    } else {
+        // many (mostly empty) runs: each lane searches the tables directly
+#pragma unroll 1
+        for (int j = 0; j < GK; ++j) {
+            const uint32_t p = pw + (uint32_t)j * WAVE;
+            if (p < nvalid) {
+                const uint32_t P = L0 + p;
+                uint32_t lo = e0, hi = e1 + 1;  // ls[lo] <= P < ls[hi]
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (tb.ls[mid] <= P) lo = mid;
+                    else hi = mid;
+                }
+                k[j] = src[tb.sr[lo] + (P - tb.ls[lo])];
+            } else {
+                k[j] = sentinel;
+            }
+        }
+    }
+}
+
+struct GsSmem {
+    union {  // the run tables are only read while the tile is gathered, before the reorder
+        uint32_t keys[GT];
+        GsRuns g;
+    };
+    uint32_t wh[GW * 256];
+    uint32_t probe[WAVE];
+    uint32_t wsum[8];
+    uint32_t mm[GW][8];
+    uint32_t ordered;
+};
+
+// One pass: gather (or, for the input, load) tile T, sort it by digit `pass` in LDS,
+// write it contiguously to the other buffer, record its digit counts and offsets.
+__global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *__restrict__ in, uint32_t *bufA, uint32_t *bufB,
+                                                  GsTables tA, GsTables tB, uint32_t *__restrict__ rt,
+                                                  uint32_t *__restrict__ mm, GsState *st, int pass, uint32_t n,
+                                                  uint32_t ntp, uint32_t flip) {
+    if (!gs_active(st, pass)) return;
+    const uint32_t T = gs_tile(blockIdx.x, ntp);
+    if (T >= ntp) return;
+    __shared__ GsSmem sm;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t cur = st->cur;
+    const uint32_t *src = cur == 0 ? in : cur == 1 ? bufA : bufB;
+    uint32_t *dst = cur == 1 ? bufB : bufA;
+    const uint32_t L0 = T * (uint32_t)GT;
+    const uint32_t nvalid = (n - L0) < (uint32_t)GT ? (n - L0) : (uint32_t)GT;
+    const uint32_t sentinel = ~flip;  // digit 255 in every pass: ranks after all real keys
+    const uint32_t shift = (uint32_t)pass * 8u;
+
+    for (uint32_t i = tid; i < (uint32_t)(GW * 256); i += GB) sm.wh[i] = 0u;
+    if (wid == 0) {
+        const bool ord = lds_lane_ordered(sm.probe, lane);
+        if (lane == 0) sm.ordered = ord ? 1u : 0u;
+    }
+    uint32_t k[GK];
+    if (cur == 0) {
+        const uint32_t *s = src + L0 + wid * (GK * WAVE) + lane;
+        const uint32_t woff = wid * (GK * WAVE) + lane;
+        if (nvalid == (uint32_t)GT) {
+#pragma unroll
+            for (int j = 0; j < GK; ++j) k[j] = s[j * WAVE];
+        } else {
+#pragma unroll
+            for (int j = 0; j < GK; ++j) k[j] = woff + j * WAVE < nvalid ? s[j * WAVE] : sentinel;
+        }
+        __syncthreads();
+    } else {
+        gs_gather(src, cur == 1 ? tA : tB, T, L0, nvalid, sentinel, sm.g, k, tid, lane, wid);
+        __syncthreads();
+    }
+    const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
+
+    // stable wave rank (slot-major order = position order), two 16-bit ranks per register
+    uint32_t *wh = sm.wh + wid * 256;
+    uint32_t rk[GK / 2];
+#pragma unroll
+    for (int j = 0; j < GK; ++j) {
+        const uint32_t d = ((k[j] ^ flip) >> shift) & 255u;
+        uint32_t r;
+        if (atomic_rank) {
+            r = __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        } else {
+            const uint64_t m = match8(d);
+            const uint32_t pre = mbcnt64(m);
+            const uint32_t old = wh[d];
+            if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
+            r = old + pre;
+        }
+        rk[j / 2] = (j & 1) ? rk[j / 2] | (r << 16) : r;
+    }
+    // pass 0: digit min / max over the valid keys (for the later passes' skip test)
+    if (pass == 0) {
+        uint32_t mn = 0xFFFFFFFFu, mx = 0u;  // bytes: digits 0..3 of (key ^ flip)
+        uint32_t mnb[4] = {255u, 255u, 255u, 255u}, mxb[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int j = 0; j < GK; ++j) {
+            if (wid * (GK * WAVE) + j * WAVE + lane < nvalid) {
+                const uint32_t v = k[j] ^ flip;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t b = (v >> (8 * q)) & 255u;
+                    mnb[q] = b < mnb[q] ? b : mnb[q];
+                    mxb[q] = b > mxb[q] ? b : mxb[q];
+                }
+            }
+        }
+        mn = mnb[0] | (mnb[1] << 8) | (mnb[2] << 16) | (mnb[3] << 24);
+        mx = mxb[0] | (mxb[1] << 8) | (mxb[2] << 16) | (mxb[3] << 24);
+        // per-byte min / max across the wave
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const uint32_t omn = __shfl_xor(mn, off), omx = __shfl_xor(mx, off);
+            uint32_t a = 0, b = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t x = (mn >> (8 * q)) & 255u, y = (omn >> (8 * q)) & 255u;
+                const uint32_t u = (mx >> (8 * q)) & 255u, w = (omx >> (8 * q)) & 255u;
+                a |= (x < y ? x : y) << (8 * q);
+                b |= (u > w ? u : w) << (8 * q);
+            }
+            mn = a;
+            mx = b;
+        }
+        if (lane == 0) {
+            sm.mm[wid][0] = mn;
+            sm.mm[wid][1] = mx;
+        }
+    }
+    __syncthreads();  // (1) wave counts
+
+    // tile histogram, local digit offsets, per-wave offsets
+    uint32_t tot = 0;
+    if (tid < 256u) {
+#pragma unroll
+        for (int w = 0; w < GW; ++w) tot += sm.wh[w * 256 + tid];
+    }
+    const uint32_t ds = block_excl_scan<GB, 256>(tot, sm.wsum);
+    if (tid < 256u) {
+        uint32_t run = ds;
+#pragma unroll
+        for (int w = 0; w < GW; ++w) {
+            const uint32_t c = sm.wh[w * 256 + tid];
+            sm.wh[w * 256 + tid] = run;
+            run += c;
+        }
+        const uint32_t cnt = tid == 255u ? tot - ((uint32_t)GT - nvalid) : tot;  // drop sentinels
+        rt[(size_t)T * 256 + tid] = ds | (cnt << 16);
+    }
+    if (pass == 0 && tid == 0) {
+        uint32_t mn = sm.mm[0][0], mx = sm.mm[0][1];
+        for (int w = 1; w < GW; ++w) {
+            uint32_t a = 0, b = 0;
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t x = (mn >> (8 * q)) & 255u, y = (sm.mm[w][0] >> (8 * q)) & 255u;
+                const uint32_t u = (mx >> (8 * q)) & 255u, v = (sm.mm[w][1] >> (8 * q)) & 255u;
+                a |= (x < y ? x : y) << (8 * q);
+                b |= (u > v ? u : v) << (8 * q);
+            }
+            mn = a;
+            mx = b;
+        }
+        mm[2 * T] = mn;
+        mm[2 * T + 1] = mx;
+    }
+    __syncthreads();  // (2) wave offsets
+
+    // reorder into LDS, then write the tile contiguously (whole lines)
+#pragma unroll
+    for (int j = 0; j < GK; ++j) {
+        const uint32_t d = ((k[j] ^ flip) >> shift) & 255u;
+        sm.keys[wh[d] + ((rk[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = k[j];
+    }
+    __syncthreads();  // (3) tile sorted in LDS
+    if (nvalid == (uint32_t)GT) {
+        const uint4 *s4 = reinterpret_cast<const uint4 *>(sm.keys);
+        uint4 *d4 = reinterpret_cast<uint4 *>(dst + L0);
+#pragma unroll
+        for (int j = 0; j < GK / 4; ++j) d4[j * GB + tid] = s4[j * GB + tid];
+    } else {
+#pragma unroll
+        for (int j = 0; j < GK; ++j) {
+            const uint32_t i = (uint32_t)j * GB + tid;
+            if (i < nvalid) dst[L0 + i] = sm.keys[i];
+        }
+    }
+}
+
+// ---- scan of the tile rows ------------------------------------------------------------
+// k_gsum: column sums of GS_GROUP consecutive tiles' counts (and, after pass 0, their
+// digit min / max).
+__global__ __launch_bounds__(256) void k_gsum(const uint32_t *__restrict__ rt, const uint32_t *__restrict__ mm,
+                                              uint32_t *__restrict__ gsum, uint32_t *__restrict__ gmm,
+                                              const GsState *st, int pass, uint32_t ntp) {
+    if (!gs_active(st, pass)) return;
+    const uint32_t g = blockIdx.x, d = threadIdx.x;
+    const uint32_t t0 = g * GS_GROUP, t1 = t0 + GS_GROUP < ntp ? t0 + GS_GROUP : ntp;
+    uint32_t h = 0;
+#pragma unroll 8
+    for (uint32_t t = t0; t < t1; ++t) h += rt[(size_t)t * 256 + d] >> 16;
+    gsum[(size_t)g * 256 + d] = h;
+    if (pass == 0 && d < 4u) {
+        uint32_t mn = 255u, mx = 0u;
+        for (uint32_t t = t0; t < t1; ++t) {
+            const uint32_t a = (mm[2 * t] >> (8 * d)) & 255u, b = (mm[2 * t + 1] >> (8 * d)) & 255u;
+            mn = a < mn ? a : mn;
+            mx = b > mx ? b : mx;
+        }
+        gmm[g * 8 + d] = mn;
+        gmm[g * 8 + 4 + d] = mx;
+    }
+}
+
+// k_gscan (one workgroup per digit d): exclusive scan of digit d's group sums over the
+// groups, and d's total; workgroup 0 then moves the current logical order to this
+// pass's output buffer and, after pass 0, reduces the digit min / max.
+__global__ __launch_bounds__(1024) void k_gscan(const uint32_t *__restrict__ gsum, uint32_t *__restrict__ gsx,
+                                                uint32_t *__restrict__ tot, const uint32_t *__restrict__ gmm,
+                                                GsState *st, int pass, uint32_t ngroups, uint32_t n, uint32_t ntp,
+                                                GsTables tA, GsTables tB) {
+    if (!gs_active(st, pass)) return;
+    __shared__ uint32_t wsum[16];
+    const uint32_t tid = threadIdx.x, d = blockIdx.x;
+    constexpr int GPT = 4;  // groups per thread: ngroups <= 4096 (2^35 keys)
+    uint32_t v[GPT], s = 0;
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) {
+        const uint32_t g = tid * GPT + i;
+        v[i] = g < ngroups ? gsum[(size_t)g * 256 + d] : 0u;
+        s += v[i];
+    }
+    uint32_t run = block_excl_scan<1024, 1024>(s, wsum);
+#pragma unroll
+    for (int i = 0; i < GPT; ++i) {
+        const uint32_t g = tid * GPT + i;
+        if (g < ngroups) gsx[(size_t)g * 256 + d] = run;
+        run += v[i];
+    }
+    if (tid == 1023) tot[d] = run;
+    if (d == 0 && tid == 0) {
+        const uint32_t nxt = st->cur == 1 ? 2u : 1u;
+        (nxt == 1 ? tA : tB).ls[(size_t)256 * ntp] = n;  // sentinel start after the last run
+        st->cur = nxt;
+    }
+    if (d == 0 && pass == 0 && tid < 4u) {
+        uint32_t mn = 255u, mx = 0u;
+        for (uint32_t g = 0; g < ngroups; ++g) {
+            mn = gmm[g * 8 + tid] < mn ? gmm[g * 8 + tid] : mn;
+            mx = gmm[g * 8 + 4 + tid] > mx ? gmm[g * 8 + 4 + tid] : mx;
+        }
+        st->dmin[tid] = mn;
+        st->dmax[tid] = mx;
+    }
+}
+
+// k_gout: the tables of this pass's output buffer (now st->cur), GS_GROUP tiles per
+// workgroup (4 threads per digit, 16 tiles each); digit-major writes go through LDS so
+// each is a 256-B line segment.
+__global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, const uint32_t *__restrict__ gsx,
+                                               const uint32_t *__restrict__ tot, GsTables tA, GsTables tB,
+                                               const GsState *st, int pass, uint32_t ntp, uint32_t n) {
+    if (!gs_active(st, pass)) return;
+    __shared__ uint32_t lsb[GS_GROUP][257], srb[GS_GROUP][257];
+    __shared__ uint32_t part[4][256];
+    __shared__ uint32_t wsum[16];
+    const GsTables tb = st->cur == 1 ? tA : tB;
+    const uint32_t g = blockIdx.x, tid = threadIdx.x, d = tid & 255u, q = tid >> 8;
+    constexpr int TPQ = GS_GROUP / 4;
+    const uint32_t t0 = g * GS_GROUP + q * TPQ;
+    uint32_t w[TPQ], h = 0;
+#pragma unroll
+    for (int i = 0; i < TPQ; ++i) {
+        w[i] = t0 + i < ntp ? rt[(size_t)(t0 + i) * 256 + d] : 0u;
+        h += w[i] >> 16;
+    }
+    part[q][d] = h;
+    // global exclusive digit offsets from the digit totals
+    const uint32_t gx = block_excl_scan<1024, 256>(q == 0 ? tot[d] : 0u, wsum);
+    __shared__ uint32_t gxs[256];
+    if (q == 0) gxs[d] = gx;
+    __syncthreads();
+    uint32_t run = gxs[d] + gsx[(size_t)g * 256 + d];
+    for (uint32_t r = 0; r < q; ++r) run += part[r][d];
+#pragma unroll
+    for (int i = 0; i < TPQ; ++i) {
+        const uint32_t t = t0 + i;
+        const uint32_t hh = w[i] >> 16, ls = run;
+        run += hh;
+        lsb[q * TPQ + i][d] = ls;
+        srb[q * TPQ + i][d] = t * (uint32_t)GT + (w[i] & 0xFFFFu);
+        if (hh && t < ntp) {
+            const uint32_t e = d * ntp + t;
+            for (uint32_t T = (ls + GT - 1) / GT; T < ntp && (uint64_t)T * GT < (uint64_t)ls + hh; ++T) tb.first[T] = e;
+            if (ls <= n - 1 && n - 1 < ls + hh) tb.first[ntp] = e;
+        }
+    }
+    __syncthreads();
+    const uint32_t lane = tid & 63u, wv = tid >> 6;
+    const uint32_t tg = g * GS_GROUP + lane;
+    if (tg < ntp) {
+        for (uint32_t dd = wv; dd < 256u; dd += 16u) {
+            tb.ls[(size_t)dd * ntp + tg] = lsb[lane][dd];
+            tb.sr[(size_t)dd * ntp + tg] = srb[lane][dd];
+        }
+    }
+}
+
+// Final pass: the logical order after the last pass, gathered and written to `out`.
+__global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gcopy(const uint32_t *__restrict__ bufA, const uint32_t *__restrict__ bufB,
+                                                 GsTables tA, GsTables tB, const GsState *st,
+                                                 uint32_t *__restrict__ out, uint32_t n, uint32_t ntp) {
+    const uint32_t T = gs_tile(blockIdx.x, ntp);
+    if (T >= ntp) return;
+    __shared__ GsRuns g;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t cur = st->cur;
+    const uint32_t L0 = T * (uint32_t)GT;
+    const uint32_t nvalid = (n - L0) < (uint32_t)GT ? (n - L0) : (uint32_t)GT;
+    uint32_t k[GK];
+    gs_gather(cur == 1 ? bufA : bufB, cur == 1 ? tA : tB, T, L0, nvalid, 0u, g, k, tid, lane, wid);
+    uint32_t *o = out + L0 + wid * (GK * WAVE) + lane;
+    const uint32_t woff = wid * (GK * WAVE) + lane;
+#pragma unroll
+    for (int j = 0; j < GK; ++j)
+        if (woff + j * WAVE < nvalid) o[j * WAVE] = k[j];
+}
+
+inline size_t al(size_t x) { return (x + 65535) / 65536 * 65536; }
+
+}  // namespace
+
+// ---- host side -------------------------------------------------------------------------
+GsLayout gs_layout(size_t n) {
+    GsLayout L{};
+    const size_t ntp = (n + GT - 1) / GT, ng = (ntp + GS_GROUP - 1) / GS_GROUP, ne = 256 * ntp;
+    size_t o = 0;
+    L.off_state = o;
+    o = al(o + 512);
+    L.off_a = o;
+    o = al(o + n * 4);
+    L.off_b = o;
+    o = al(o + n * 4);
+    L.off_rt = o;
+    o = al(o + ne * 4);
+    L.off_mm = o;
+    o = al(o + ntp * 8);
+    L.off_gsum = o;
+    o = al(o + ng * 256 * 4);
+    L.off_gsx = o;
+    o = al(o + ng * 256 * 4);
+    L.off_gx = o;
+    o = al(o + 257 * 4);
+    L.off_gmm = o;
+    o = al(o + ng * 8 * 4);
+    for (int s = 0; s < 2; ++s) {
+        L.off_ls[s] = o;
+        o = al(o + (ne + 1) * 4);
+        L.off_sr[s] = o;
+        o = al(o + ne * 4);
+        L.off_first[s] = o;
+        o = al(o + (ntp + 1) * 4);
+    }
+    L.total = o;
+    return L;
+}
+
+hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s,
+                              const GsHooks &hooks) {
+    const GsLayout L = gs_layout(n);
+    const uint32_t ntp = (uint32_t)((n + GT - 1) / GT), ng = (ntp + GS_GROUP - 1) / GS_GROUP;
+    GsState *st = reinterpret_cast<GsState *>(ws + L.off_state);
+    uint32_t *A = reinterpret_cast<uint32_t *>(ws + L.off_a), *B = reinterpret_cast<uint32_t *>(ws + L.off_b);
+    uint32_t *rt = reinterpret_cast<uint32_t *>(ws + L.off_rt), *mm = reinterpret_cast<uint32_t *>(ws + L.off_mm);
+    uint32_t *gsum = reinterpret_cast<uint32_t *>(ws + L.off_gsum), *gsx = reinterpret_cast<uint32_t *>(ws + L.off_gsx);
+    uint32_t *gx = reinterpret_cast<uint32_t *>(ws + L.off_gx), *gmm = reinterpret_cast<uint32_t *>(ws + L.off_gmm);
+    GsTables t[2];
+    for (int i = 0; i < 2; ++i)
+        t[i] = GsTables{reinterpret_cast<uint32_t *>(ws + L.off_ls[i]), reinterpret_cast<uint32_t *>(ws + L.off_sr[i]),
+                        reinterpret_cast<uint32_t *>(ws + L.off_first[i])};
+    hipError_t e = hipMemsetAsync(ws + L.off_state, 0, 512, s);
+    if (e != hipSuccess) return e;
+    const unsigned grid = 8u * ((ntp + 7u) / 8u);
+    for (int p = 0; p < 4; ++p) {
+        if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GSWEEP, s);
+        k_gsweep<<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, mm, st, p, (uint32_t)n, ntp, flip);
+        if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        k_gsum<<<ng, 256, 0, s>>>(rt, mm, gsum, gmm, st, p, ntp);
+        k_gscan<<<256, 1024, 0, s>>>(gsum, gsx, gx, gmm, st, p, ng, (uint32_t)n, ntp, t[0], t[1]);
+        k_gout<<<ng, 1024, 0, s>>>(rt, gsx, gx, t[0], t[1], st, p, ntp, (uint32_t)n);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GCOPY, s);
+    k_gcopy<<<grid, GB, 0, s>>>(A, B, t[0], t[1], st, out, (uint32_t)n, ntp);
+    if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GCOPY, s);
+    return hipGetLastError();
+}
+
+}  // namespace labsort

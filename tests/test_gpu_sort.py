@@ -306,8 +306,10 @@ def test_count_descents(ls, oracle, torch_gpu):
     assert int(c.item()) == 3
 
 
-def test_timing_hooks(ls, oracle, torch_gpu):
+@pytest.mark.parametrize("impl", ["gather", "onesweep"])
+def test_timing_hooks(ls, oracle, torch_gpu, monkeypatch, impl):
     torch = torch_gpu
+    monkeypatch.setenv("LABSORT_RADIX_IMPL", impl)
     n = 1 << 20
     t = torch.empty(n, dtype=torch.int32, device="cuda")
     ls.fill(t, n, SEED, "u32")
@@ -315,9 +317,11 @@ def test_timing_hooks(ls, oracle, torch_gpu):
     ls.timing_enable(True)
     ls.sort_device(t, o, n, algo="radix")
     torch.cuda.synchronize()
-    ms, cnt = ls.timing_read("onesweep")
+    ms, cnt = ls.timing_read("gsweep" if impl == "gather" else "onesweep")
+    ms2, cnt2 = ls.timing_read("gcopy")
     ls.timing_enable(False)
-    assert cnt == 4 and ms > 0
+    assert cnt == 4 and ms > 0  # four 8-bit passes (gather: pass 0 always runs, 1-3 active here)
+    assert cnt2 == (1 if impl == "gather" else 0)
 
 
 # ---- segmented look-back chains: pass structure edge cases ----------------------------

@@ -34,7 +34,7 @@ print("ok")
 
 @pytest.mark.parametrize("variant", ["00", "01", "10", "11", "20", "21"])
 def test_onesweep_variant(oracle, variant):
-    env = dict(os.environ, LABSORT_OSP=variant)
+    env = dict(os.environ, LABSORT_OSP=variant, LABSORT_RADIX_IMPL="onesweep")
     r = subprocess.run([sys.executable, "-c", SCRIPT, REPO], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
@@ -44,7 +44,7 @@ def test_onesweep_chains(oracle, seg):
     """Every look-back chain layout (LABSORT_SEG) sorts correctly with the default
     rank: position segments in the first pass only, digit-group segments in the
     later passes too (joint histograms), one chain everywhere."""
-    env = dict(os.environ, LABSORT_SEG=seg)
+    env = dict(os.environ, LABSORT_SEG=seg, LABSORT_RADIX_IMPL="onesweep")
     env.pop("LABSORT_OSP", None)
     r = subprocess.run([sys.executable, "-c", SCRIPT, REPO], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
