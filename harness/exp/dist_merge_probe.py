@@ -1,7 +1,9 @@
 """Diagnostic: the multi-GPU exchange's merge step on one GPU.  p sorted runs of
 2^28/p keys back to back (what a rank holds after the splitter exchange), merged by
-(a) the tree of labsort_merge passes (HipOps default) and (b) one K-way pass
-(labsort_merge_runs, HipOps(kway=True)).  Median ms of 10 after warm-up."""
+(a) the Python tree of labsort_merge calls (HipOps(kway=False)), (b) labsort_merge_runs
+(HipOps default): log2 p levels of merge-path passes over explicit pairs of runs, and
+(c) labsort_merge_runs with LABSORT_MERGE_RUNS=kway (one K-way pass, kmerge.hip).
+Median ms of 10 after warm-up; the three outputs must be equal."""
 import importlib, json, os, sys, time
 R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, R)
@@ -19,7 +21,13 @@ for p in (2, 4, 8):
         ls.sort_device(buf[q * m:(q + 1) * m], buf[q * m:(q + 1) * m], m, workspace=ws)
     offs = [q * m for q in range(p + 1)]
     row = {"p": p, "n": n}
-    for kway in (False, True):
+    outs = []
+    for mode in ("tree", "passes", "kway"):
+        kway = mode != "tree"
+        if mode == "kway":
+            os.environ["LABSORT_MERGE_RUNS"] = "kway"
+        else:
+            os.environ.pop("LABSORT_MERGE_RUNS", None)
         ops = D.HipOps(ls, kway=kway)
         for _ in range(2):
             ops.merge_runs(buf, offs)
@@ -31,5 +39,7 @@ for p in (2, 4, 8):
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) * 1e3)
         ts.sort()
-        row["kway_ms" if kway else "tree_ms"] = round(ts[len(ts) // 2], 3)
+        row[mode + "_ms"] = round(ts[len(ts) // 2], 3)
+        outs.append(out.clone())
+    row["equal"] = bool(torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2]))
     print(json.dumps(row), flush=True)

@@ -529,7 +529,10 @@ int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *
     return LABSORT_OK;
 }
 
-size_t labsort_merge_runs_workspace_bytes(size_t n) { return km_workspace_words(n) * 4; }
+size_t labsort_merge_runs_workspace_bytes(size_t n) {
+    const size_t km = km_workspace_words(n) * 4, tree = align_up(n * 4, 256);  // K-way cuts | ping-pong keys
+    return km > tree ? km : tree;
+}
 
 int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, int nruns, int key_type,
                        void *d_ws, size_t ws_bytes, void *stream) {
@@ -546,6 +549,43 @@ int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, i
     if (nruns == 1) {
         HIP_TRY(hipMemcpyAsync(static_cast<uint32_t *>(d_out) + h_offsets[0],
                                static_cast<const uint32_t *>(d_in) + h_offsets[0], n * 4, hipMemcpyDeviceToDevice, s));
+        return LABSORT_OK;
+    }
+    const char *impl = std::getenv("LABSORT_MERGE_RUNS");
+    if (!(impl && !std::strcmp(impl, "kway"))) {
+        // log2(nruns) levels of pairwise merge-path passes over explicit pairs of runs
+        // (k_merge_pass_p, one launch per pair), ping-ponging through the workspace so
+        // that the last level writes d_out
+        const uint32_t *src = static_cast<const uint32_t *>(d_in) + h_offsets[0];
+        uint32_t *outp = static_cast<uint32_t *>(d_out) + h_offsets[0];
+        uint32_t *tmp = static_cast<uint32_t *>(d_ws);
+        std::vector<size_t> o(h_offsets, h_offsets + nruns + 1);
+        for (auto &x : o) x -= h_offsets[0];
+        int levels = 0;
+        while ((1 << levels) < nruns) ++levels;
+        const uint32_t flip = flip_of(key_type);
+        TimingScope ts(LABSORT_K_MERGE, s);
+        for (int l = 0; l < levels; ++l) {
+            uint32_t *dst = ((levels - 1 - l) % 2 == 0) ? outp : tmp;
+            std::vector<size_t> no;
+            for (size_t i = 0; i + 1 < o.size(); i += 2) {
+                const size_t a0 = o[i], a1 = o[i + 1], b1 = i + 2 < o.size() ? o[i + 2] : a1;
+                no.push_back(a0);
+                if (b1 == a1) {  // no partner: carried over
+                    if (a1 > a0) HIP_TRY(hipMemcpyAsync(dst + a0, src + a0, (a1 - a0) * 4, hipMemcpyDeviceToDevice, s));
+                    continue;
+                }
+                MgPairs pr{};
+                pr.np = 1;
+                pr.pb[0] = 0;
+                pr.pb[1] = (uint32_t)(b1 - a0);
+                pr.la[0] = (uint32_t)(a1 - a0);
+                HIP_TRY(launch_merge_pass(src + a0, dst + a0, b1 - a0, 0, flip, nullptr, s, nullptr, nullptr, &pr));
+            }
+            no.push_back(o.back());
+            o.swap(no);
+            src = dst;
+        }
         return LABSORT_OK;
     }
     KmRuns rs{};

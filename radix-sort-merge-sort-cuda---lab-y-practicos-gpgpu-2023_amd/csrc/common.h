@@ -113,6 +113,15 @@ constexpr int MG_BLOCK = LABSORT_MG_BLOCK;  // r15 sweep: 512 x 8 keys (4096-key
 constexpr int MG_KPT = LABSORT_MG_KPT;
 constexpr int MG_TILE = MG_BLOCK * MG_KPT;
 constexpr int MG_MAX_TPB = 256;       // most consecutive output tiles per merge workgroup
+constexpr int MG_MAX_PAIRS = 4;       // explicit pairs of runs per merge level (up to 8 runs)
+// One merge level over explicit runs: pair i = runs A = [pb[i], pb[i] + la[i]) and
+// B = [pb[i] + la[i], pb[i+1]) merged in place of the pair (labsort_merge_runs); np = 0:
+// uniform runs of `run` keys (the merge sort's passes)
+struct MgPairs {
+    uint32_t np;
+    uint32_t pb[MG_MAX_PAIRS + 1];
+    uint32_t la[MG_MAX_PAIRS];
+};
 #ifndef LABSORT_MG_BRACKET
 #define LABSORT_MG_BRACKET 8
 #endif
@@ -237,7 +246,8 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t run, uint32_t flip,
-                             uint32_t *part, hipStream_t s, const uint32_t *vin = nullptr, uint32_t *vout = nullptr);
+                             uint32_t *part, hipStream_t s, const uint32_t *vin = nullptr, uint32_t *vout = nullptr,
+                             const MgPairs *pairs = nullptr);
 hipError_t launch_tile_sort_kv(const uint32_t *in, uint32_t *out, const uint32_t *vin, uint32_t *vout, size_t n,
                                uint32_t flip, hipStream_t s);
 hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size_t lb, uint32_t *out, size_t d0,

@@ -1223,8 +1223,18 @@ __device__ __forceinline__ void merge_tile(const uint32_t *__restrict__ A, uint3
 struct PairGeom {
     uint32_t pb, la, lb;
 };
-__device__ __forceinline__ PairGeom pair_of(uint32_t o, uint32_t n, uint32_t run) {
+__device__ __forceinline__ PairGeom pair_of(uint32_t o, uint32_t n, uint32_t run, const MgPairs &pr) {
     PairGeom g;
+    if (pr.np) {  // explicit pairs: the one holding output position o
+        uint32_t i = 0;
+#pragma unroll
+        for (int q = 1; q < MG_MAX_PAIRS; ++q)
+            if ((uint32_t)q < pr.np && o >= pr.pb[q]) i = (uint32_t)q;
+        g.pb = pr.pb[i];
+        g.la = pr.la[i];
+        g.lb = pr.pb[i + 1] - pr.pb[i] - pr.la[i];
+        return g;
+    }
     g.pb = (o / (2u * run)) * (2u * run);
     const uint32_t rest = n - g.pb;
     g.la = rest < run ? rest : run;
@@ -1242,7 +1252,7 @@ __device__ __forceinline__ PairGeom pair_of(uint32_t o, uint32_t n, uint32_t run
 template <int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                         uint32_t n, uint32_t run, uint32_t flip, uint32_t ntiles,
-                                                        uint32_t m, const uint32_t *__restrict__ vsrc = nullptr,
+                                                        uint32_t m, MgPairs pr, const uint32_t *__restrict__ vsrc = nullptr,
                                                         uint32_t *__restrict__ vdst = nullptr) {
     constexpr uint32_t T = (uint32_t)(BLOCK * KPT);
     static_assert(T == (uint32_t)MG_TILE, "tile granularity");
@@ -1263,16 +1273,16 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
     auto search = [&](uint32_t i, uint32_t S) {
         const uint32_t o = (t0 + i) * T;
         if (o >= n) return 0u;
-        const PairGeom g = pair_of(o, n, run);
+        const PairGeom g = pair_of(o, n, run, pr);
         uint32_t lo = 0u, hi = ~0u;
         if (S) {
             const uint32_t il = i - i % S, ih = il + S < nb ? il + S : nb;
             const uint32_t ol = (t0 + il) * T, oh = (t0 + ih) * T;
-            if (pair_of(ol, n, run).pb == g.pb) {
+            if (pair_of(ol, n, run, pr).pb == g.pb) {
                 lo = s_part[il];
                 hi = lo + (o - ol);
             }
-            if (oh < n && pair_of(oh, n, run).pb == g.pb) {
+            if (oh < n && pair_of(oh, n, run, pr).pb == g.pb) {
                 const uint32_t ah = s_part[ih];
                 hi = hi < ah ? hi : ah;
                 if (ah > oh - o && lo < ah - (oh - o)) lo = ah - (oh - o);
@@ -1293,7 +1303,7 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         Geo q;
         q.o0 = t * T;
         const uint32_t o1 = (n - q.o0) < T ? n : q.o0 + T;
-        const PairGeom g = pair_of(q.o0, n, run);
+        const PairGeom g = pair_of(q.o0, n, run, pr);
         const uint32_t a0 = s_part[t - t0];
         const uint32_t a1 = (o1 - g.pb == g.la + g.lb) ? g.la : s_part[t + 1 - t0];
         const uint32_t b0 = (q.o0 - g.pb) - a0;
@@ -1590,7 +1600,9 @@ hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStr
 }
 
 hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t run, uint32_t flip,
-                             uint32_t *part, hipStream_t s, const uint32_t *vin, uint32_t *vout) {
+                             uint32_t *part, hipStream_t s, const uint32_t *vin, uint32_t *vout, const MgPairs *pairs) {
+    MgPairs pr{};
+    if (pairs) pr = *pairs;
     if (n == 0) return hipSuccess;
     (void)part;  // co-ranks are found inside k_merge_pass_p
     const uint32_t ntiles = (uint32_t)((n + MG_TILE - 1) / MG_TILE);
@@ -1600,9 +1612,9 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
     const uint32_t g = (ntiles + m - 1) / m;
     if (vin)
         k_merge_pass_p<MG_BLOCK, MG_KPT, true>
-            <<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, vin, vout);
+            <<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr, vin, vout);
     else
-        k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m);
+        k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr);
     return hipGetLastError();
 }
 
