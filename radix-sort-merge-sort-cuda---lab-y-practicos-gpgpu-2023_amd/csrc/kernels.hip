@@ -1085,22 +1085,29 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
             rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
         }
         __syncthreads();
+        // tile-wide digit offsets folded into the per-wave offsets: the reorder then
+        // reads one LDS word per key instead of two (LDS was busy 68 % of the kernel,
+        // 60 % of it bank conflicts: profiles/r17_pmc_tile_sort.txt)
         uint32_t tot = 0;
         if (tid < (uint32_t)R) {
 #pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint32_t c = sm.whist[w * R + tid];
-                sm.whist[w * R + tid] = tot;
-                tot += c;
-            }
+            for (int w = 0; w < W; ++w) tot += sm.whist[w * R + tid];
         }
         const uint32_t ds = block_excl_scan<BLOCK, R>(tot, sm.wsum);
-        if (tid < (uint32_t)R) sm.dstart[tid] = ds;
+        if (tid < (uint32_t)R) {
+            uint32_t run = ds;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint32_t c = sm.whist[w * R + tid];
+                sm.whist[w * R + tid] = run;
+                run += c;
+            }
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-            const uint32_t dst = sm.dstart[d] + wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
+            const uint32_t dst = wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
             sm.keys[dst] = k[j];
             if constexpr (KV) sm.vals[dst] = v[j];
         }
