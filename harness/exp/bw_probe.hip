@@ -230,6 +230,39 @@ __global__ __launch_bounds__(1024) void k_gather(const uint32_t *a, uint32_t *b,
         }
     }
 }
+// padded scatter: tile t writes 256 runs of RUN words, run (t, d) at a 16-word-aligned
+// slot of SLOT words (SLOT - RUN words of padding nobody writes); GATHER: the tile's
+// keys are also read as runs of RUN words from such a padded layout (the next pass of
+// a padded design), else read contiguously
+template <int RUN, int SLOT, int GATHER>
+__global__ __launch_bounds__(1024) void k_padded(const uint32_t *a, uint32_t *b, uint32_t ntiles) {
+    const uint32_t tid = threadIdx.x;
+    const size_t region = (size_t)ntiles * SLOT;
+    const uint32_t g = blockIdx.x & 7u, per = ntiles / 8u;
+    constexpr uint32_t TK = 256 * RUN;  // keys per tile
+    for (uint32_t q = blockIdx.x >> 3; q < per; q += gridDim.x >> 3) {
+        const uint32_t t = g * per + q;
+        uint32_t k[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t i = j * 1024 + tid;
+            if (i < TK) {
+                if (GATHER) {
+                    // logical position L = t*TK + i: bucket d = L / (ntiles*RUN), run tt, word u
+                    const size_t L = (size_t)t * TK + i, d = L / ((size_t)ntiles * RUN), r = L % ((size_t)ntiles * RUN);
+                    k[j] = a[d * region + (r / RUN) * SLOT + r % RUN];
+                } else {
+                    k[j] = a[(size_t)t * TK + i];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t i = j * 1024 + tid;
+            if (i < TK) b[(i / RUN) * region + (size_t)t * SLOT + i % RUN] = k[j];
+        }
+    }
+}
 // MODE 0: aligned runs of 64; 1: runs shifted by a per-(t,d) offset (region stride has
 // 64 words of slack per tile); 2: variable run lengths (lens[t*256+d], prefix offs).
 template <int MODE>
@@ -422,6 +455,26 @@ int main() {
     printf("run-64 K8cv   %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
     t = timeit([&] { k_abut_run<64, 16, 1, 1><<<256, 1024>>>(in, out, ntiles); });
     printf("run-64 K16cv  %.4f ms  %7.1f GB/s\n", t, gb / t * 1e3);
+    {
+        uint32_t *pa, *pb;
+        const size_t words = (size_t)ntiles * 256 * 80 + 4096;
+        CK(hipMalloc(&pa, words * 4));
+        CK(hipMalloc(&pb, words * 4));
+        CK(hipMemset(pa, 1, words * 4));
+        auto rate = [&](double keys, float ms) { return 8.0 * keys / 1e9 / ms * 1e3; };
+        t = timeit([&] { k_padded<64, 64, 0><<<256, 1024>>>(pa, pb, ntiles); });
+        printf("pad-64/64      %.4f ms  %7.1f GB/s (aligned runs, no padding)\n", t, rate(256.0 * 64 * ntiles, t));
+        t = timeit([&] { k_padded<56, 64, 0><<<256, 1024>>>(pa, pb, ntiles); });
+        printf("pad-56/64      %.4f ms  %7.1f GB/s (aligned runs, unshared partial tails)\n", t, rate(256.0 * 56 * ntiles, t));
+        t = timeit([&] { k_padded<60, 64, 0><<<256, 1024>>>(pa, pb, ntiles); });
+        printf("pad-60/64      %.4f ms  %7.1f GB/s\n", t, rate(256.0 * 60 * ntiles, t));
+        t = timeit([&] { k_padded<56, 64, 1><<<256, 1024>>>(pa, pb, ntiles); });
+        printf("pad-56/64 gath %.4f ms  %7.1f GB/s (padded runs gathered + padded scatter)\n", t, rate(256.0 * 56 * ntiles, t));
+        t = timeit([&] { k_padded<60, 64, 1><<<256, 1024>>>(pa, pb, ntiles); });
+        printf("pad-60/64 gath %.4f ms  %7.1f GB/s\n", t, rate(256.0 * 60 * ntiles, t));
+        CK(hipFree(pa));
+        CK(hipFree(pb));
+    }
     {
         uint32_t *src2;
         CK(hipMalloc(&src2, (size_t)ntiles * (16384 + 32) * 4 + 4096));

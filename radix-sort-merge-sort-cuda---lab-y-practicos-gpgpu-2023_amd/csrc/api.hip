@@ -192,7 +192,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
     if (bits == 8) {
         // histograms first; the look-back words (tens of MB) are cleared after the
         // histogram so their dirty lines do not compete with its read of the keys
-        HIP_TRY(hipMemsetAsync(ws, 0, L.off_lookback, s));
+        HIP_TRY(launch_zero(ws, L.off_lookback, s));
         uint32_t *hps = reinterpret_cast<uint32_t *>(ws + L.off_hps);
         uint32_t *joint = reinterpret_cast<uint32_t *>(ws + L.off_joint);
         SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
@@ -200,7 +200,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
             HIP_TRY(launch_hist_seg(in, n, flip, hps, joint, s));
         }
-        HIP_TRY(hipMemsetAsync(ws + L.off_lookback, 0, L.zero_bytes - L.off_lookback, s));
+        HIP_TRY(launch_zero(ws + L.off_lookback, L.zero_bytes - L.off_lookback, s));
         HIP_TRY(launch_plan8(hps, joint, n, in == out ? 1 : 0, plan, sps, hist, s));
         for (int p = 0; p < L.P; ++p) {
             if (p > 0) HIP_TRY(launch_segplan(plan, p, n, hist, joint, sps, s));
@@ -209,7 +209,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
                                       counters + (size_t)p * OSP_NCTR, err, s));
         }
     } else {
-        HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes, s));
+        HIP_TRY(launch_zero(ws, L.zero_bytes, s));
         {
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
             HIP_TRY(launch_histogram(in, n, flip, bits, hist, s));
@@ -628,7 +628,7 @@ int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint3
     uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
     uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
     Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
-    HIP_TRY(hipMemsetAsync(ws, 0, L.zero_bytes, s));
+    HIP_TRY(launch_zero(ws, L.zero_bytes, s));
     {
         TimingScope ts(LABSORT_K_HISTOGRAM, s);
         HIP_TRY(launch_histogram(ki, n, flip, 8, hist, s));

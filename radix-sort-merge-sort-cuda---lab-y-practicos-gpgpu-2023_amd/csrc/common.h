@@ -262,6 +262,7 @@ bool verify_enabled();
 KeyPrint key_print(const int *a, size_t n);
 void verify_or_exit(const char *who, const int *a, size_t n, const KeyPrint &before);
 
+hipError_t launch_zero(void *p, size_t bytes, hipStream_t s);  // graph-replayable memset (16-B aligned p)
 hipError_t launch_count_descents(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *count, hipStream_t s);
 
 }  // namespace labsort

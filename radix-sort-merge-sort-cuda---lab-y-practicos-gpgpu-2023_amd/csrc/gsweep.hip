@@ -518,7 +518,7 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
     for (int i = 0; i < 2; ++i)
         t[i] = GsTables{reinterpret_cast<uint32_t *>(ws + L.off_ls[i]), reinterpret_cast<uint32_t *>(ws + L.off_sr[i]),
                         reinterpret_cast<uint32_t *>(ws + L.off_first[i])};
-    hipError_t e = hipMemsetAsync(ws + L.off_state, 0, 512, s);
+    hipError_t e = launch_zero(ws + L.off_state, 512, s);
     if (e != hipSuccess) return e;
     const unsigned grid = 8u * ((ntp + 7u) / 8u);
     for (int p = 0; p < 4; ++p) {

@@ -1587,6 +1587,25 @@ hipError_t launch_segplan(const Plan *plan, int pass, size_t n, const uint32_t *
     return hipGetLastError();
 }
 
+// Zero a workspace range with a kernel instead of hipMemsetAsync: the sorts' zeroing must
+// replay inside captured HIP graphs (tests/test_gpu_graph.py), which a kernel node does.
+__global__ __launch_bounds__(256) void k_zero(uint4 *__restrict__ p4, size_t n4, uint32_t *__restrict__ tail,
+                                             uint32_t ntail) {
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) p4[i] = make_uint4(0, 0, 0, 0);
+    if (blockIdx.x == 0 && threadIdx.x < ntail) tail[threadIdx.x] = 0u;
+}
+
+hipError_t launch_zero(void *p, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return hipSuccess;
+    // callers pass 4-byte multiples starting 16-byte aligned
+    const size_t n4 = bytes / 16;
+    uint32_t *tail = reinterpret_cast<uint32_t *>(static_cast<char *>(p) + n4 * 16);
+    const uint32_t ntail = (uint32_t)((bytes - n4 * 16) / 4);
+    k_zero<<<blocks_for(n4 ? n4 : 1, 256 * 4, 2048), 256, 0, s>>>(static_cast<uint4 *>(p), n4, tail, ntail);
+    return hipGetLastError();
+}
+
 hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) {
     k_final_copy<<<blocks_for(n, 256 * 16, 4096), 256, 0, s>>>(b, plan, n);
     return hipGetLastError();
