@@ -87,16 +87,22 @@ std::vector<Splitter> choose_splitters(int p, const std::vector<size_t> &m,
     return spl;
 }
 
-int make_plan(ExPlan &P, const std::vector<Splitter> &spl, uint32_t flip, const BoundFn &ub) {
-    const int p = P.p;
-    P.cut.assign((size_t)p * (p + 1), 0);
-    P.recv_off.assign((size_t)p * (p + 1), 0);
-    // values: the splitter keys, then the key just below each (its lower bound)
-    std::vector<uint32_t> vals(2 * (p - 1)), out;
+// bound-query values: the splitter keys, then the key just below each (its lower bound)
+std::vector<uint32_t> plan_values(const std::vector<Splitter> &spl, int p, uint32_t flip) {
+    std::vector<uint32_t> vals(p > 1 ? 2 * (p - 1) : 0);
     for (int j = 0; j < p - 1; ++j) {
         vals[j] = spl[j].key;
         vals[p - 1 + j] = spl[j].ord ? ((spl[j].ord - 1) ^ flip) : spl[j].key;
     }
+    return vals;
+}
+
+int make_plan(ExPlan &P, const std::vector<Splitter> &spl, uint32_t flip, const BoundFn &ub) {
+    const int p = P.p;
+    P.cut.assign((size_t)p * (p + 1), 0);
+    P.recv_off.assign((size_t)p * (p + 1), 0);
+    const std::vector<uint32_t> vals = plan_values(spl, p, flip);
+    std::vector<uint32_t> out;
     for (int r = 0; r < p; ++r) {
         size_t *c = &P.cut[(size_t)r * (p + 1)];
         c[p] = P.m[r];
@@ -372,15 +378,24 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
     // 2-3. splitters and cut points
     if (p > 1) {
         const std::vector<Splitter> spl = choose_splitters(p, P.m, samples, flip);
-        st = make_plan(P, spl, flip, [&](int r, const std::vector<uint32_t> &vals, std::vector<uint32_t> &out) -> int {
+        // every rank's bound queries at once, one host thread per rank
+        const std::vector<uint32_t> vals = plan_values(spl, p, flip);
+        std::vector<std::vector<uint32_t>> bounds(p, std::vector<uint32_t>(vals.size(), 0u));
+        st = for_ranks(p, [&](int r) -> int {
             RankState &Q = R[r];
+            if (!P.m[r]) return LABSORT_OK;
             MHIP(hipSetDevice(Q.dev));
             uint32_t *d = static_cast<uint32_t *>(Q.small.p);
             MHIP(hipMemcpyAsync(d, vals.data(), vals.size() * 4, hipMemcpyHostToDevice, Q.s));
             MHIP(launch_upper_bound(static_cast<const uint32_t *>(Q.keys.p), P.m[r], flip, d, vals.size(),
                                     d + vals.size(), Q.s));
-            MHIP(hipMemcpyAsync(out.data(), d + vals.size(), vals.size() * 4, hipMemcpyDeviceToHost, Q.s));
+            MHIP(hipMemcpyAsync(bounds[r].data(), d + vals.size(), vals.size() * 4, hipMemcpyDeviceToHost, Q.s));
             MHIP(hipStreamSynchronize(Q.s));
+            return LABSORT_OK;
+        });
+        if (st) return st;
+        st = make_plan(P, spl, flip, [&](int r, const std::vector<uint32_t> &, std::vector<uint32_t> &out) -> int {
+            out = bounds[r];
             return LABSORT_OK;
         });
         if (st) return st;
