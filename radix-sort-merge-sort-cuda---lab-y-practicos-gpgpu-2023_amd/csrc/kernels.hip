@@ -1370,6 +1370,18 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
                 vb = bi < lb ? sb[bi] : 0u;
             }
         }
+#ifndef LABSORT_MG_DIRECT
+#define LABSORT_MG_DIRECT 1
+#endif
+        if (!KV && LABSORT_MG_DIRECT && KPT % 4 == 0 && tot == T && (((uintptr_t)dst) & 15u) == 0) {
+            // a full tile: each thread's KPT outputs are consecutive, so they go straight
+            // to HBM as KPT/4 16-B stores (no LDS staging round trip, one barrier fewer)
+            uint4 *o4 = reinterpret_cast<uint4 *>(dst + cur.o0 + tid * KPT);
+#pragma unroll
+            for (int j = 0; j < KPT / 4; ++j) o4[j] = make_uint4(r[4 * j], r[4 * j + 1], r[4 * j + 2], r[4 * j + 3]);
+            cur = nxt;
+            continue;
+        }
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t idx = tid * KPT + j;
