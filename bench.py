@@ -250,6 +250,8 @@ def main():
 
     dom = "onesweep" if args.algo in ("radix", "radix1") or (args.algo == "pairs" and args.pair_algo == "radix") \
         else "merge"
+    if args.algo == "radix" and world == 1 and ls.radix_impl(n) == "gather":
+        dom = "gsweep"  # the gathered passes (2^16 <= n < 2^26)
     if world > 1:
         comm.sent_bytes, comm.p2p_rounds, comm.exchange_s = 0, 0, 0.0
         comm.timed = True
@@ -366,6 +368,35 @@ def main():
         }
         del mws, mout
 
+    # BASELINE config 2 beside the headline: 2^20 keys, radix (the gathered passes at this
+    # size), device-resident, verified; launch-bound, so reported as time per sort
+    config2 = None
+    if world == 1 and args.algo == "radix" and not args.no_merge and n > (1 << 20):
+        n2 = 1 << 20
+        s2 = torch.empty(n2, dtype=torch.int32, device=dev)
+        o2 = torch.empty_like(s2)
+        w2 = torch.empty(max(ls.workspace_bytes(n2, "radix"), 256), dtype=torch.uint8, device=dev)
+        ls.fill(s2, n2, SEED + 2, args.dist, stream=stream)
+        for _ in range(3):
+            ls.sort_device(s2, o2, n2, key=key, algo="radix", workspace=w2, stream=stream)
+        torch.cuda.synchronize()
+        reps = 50
+        c0 = time.perf_counter()
+        for _ in range(reps):
+            ls.sort_device(s2, o2, n2, key=key, algo="radix", workspace=w2, stream=stream)
+        torch.cuda.synchronize()
+        c1 = time.perf_counter()
+        ls.workspace_status(w2, n2, "radix", stream=stream)
+        ok2, _ = verify(torch, ls, s2, o2, n2, key)
+        if not ok2:
+            print("bench.py: CONFIG 2 OUTPUT CHECK FAILED", file=sys.stderr)
+            sys.exit(3)
+        config2 = {"workload": "n=2^20 uint32 radix sort, device-resident (BASELINE config 2)",
+                   "impl": ls.radix_impl(n2), "ms_per_sort": round((c1 - c0) / reps * 1e3, 4),
+                   "value": round(n2 * reps / (c1 - c0) / 1e6, 2), "unit": "Mkeys/s",
+                   "verified": "sorted permutation (descents, digit histograms, sums)"}
+        del s2, o2, w2
+
     total_keys = n * world * args.steps
     value = total_keys / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
@@ -392,6 +423,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
                     "traffic": traffic, "kernel": ("k_onesweep_p" if dom == "onesweep" and args.algo == "radix" else
+                               "k_gsweep" if dom == "gsweep" else
                                "k_onesweep<8, KV>" if args.algo == "pairs" and dom == "onesweep" else f"k_{dom}"), "launches": k_cnt,
                     "avg_launch_ms": round(avg_ms, 5) if avg_ms else None,
                     "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
@@ -425,6 +457,8 @@ def main():
         }
         if merge_leg:
             line["merge"] = merge_leg
+        if config2:
+            line["config2"] = config2
         if xgmi:
             line["config"]["local_algo"] = "radix"
             line["xgmi"] = xgmi
