@@ -25,7 +25,7 @@ CLASSES = {"k_onesweep": "onesweep", "k_histogram": "histogram", "k_hist_seg": "
            "k_km_blocks": "kmerge_blocks", "k_merge_pass": "merge",
            "k_tile_sort": "tile_sort", "k_merge_part": "partition", "k_merge_ab": "merge_ab",
            "k_count_descents": "count_descents", "k_fill": "fill", "k_final_copy": "final_copy",
-           "k_wave_split": "wave_split"}
+           "k_wave_split": "wave_split", "k_gsweep": "gsweep", "k_gcopy": "gcopy"}
 
 
 def klass(name):
