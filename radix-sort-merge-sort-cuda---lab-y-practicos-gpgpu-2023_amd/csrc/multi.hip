@@ -61,7 +61,7 @@ struct ExPlan {
 };
 
 inline size_t sample_pos(size_t m, size_t s, size_t k) { return k * m / s; }
-inline size_t samples_per_rank(int p) { return (size_t)1024 * (size_t)p; }
+inline size_t samples_per_rank(int p) { return (size_t)256 * (size_t)p; }  // ranges within ~m/(256p) keys of n/p
 
 // bound query: out[v] = number of keys of rank r's sorted shard <= values[v] (key order)
 using BoundFn = std::function<int(int r, const std::vector<uint32_t> &values, std::vector<uint32_t> &out)>;
