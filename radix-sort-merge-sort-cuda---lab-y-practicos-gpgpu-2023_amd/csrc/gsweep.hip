@@ -53,7 +53,7 @@ struct GsTables {
 // Workspace header (first 512 B; word 0 is the labsort error word, never set here)
 struct GsState {
     uint32_t err;
-    uint32_t cur;       // buffer holding the current logical order: 0 input (plain), 1 A, 2 B
+    uint32_t pad;
     uint32_t dmin[4];   // per digit, min / max over all keys (flipped digit values), from pass 0
     uint32_t dmax[4];
 };
@@ -61,6 +61,18 @@ struct GsState {
 __device__ __forceinline__ bool gs_active(const GsState *st, int pass) {
     return pass == 0 || st->dmin[pass] != st->dmax[pass];
 }
+
+// The buffer holding the logical order before pass p (0: the input, 1: A, 2: B): pass 0
+// always runs and writes A, every later active pass writes the other buffer.  A
+// function of the digit min / max only (written once, by pass 0's scan), so no kernel
+// ever updates shared "current buffer" state while others read it.
+__device__ __forceinline__ uint32_t gs_cur(const GsState *st, int p) {
+    if (p == 0) return 0u;
+    uint32_t nact = 1;
+    for (int q = 1; q < p; ++q) nact += st->dmin[q] != st->dmax[q] ? 1u : 0u;
+    return (nact & 1u) ? 1u : 2u;
+}
+__device__ __forceinline__ uint32_t gs_dst(const GsState *st, int p) { return gs_cur(st, p) == 1u ? 2u : 1u; }
 
 // tiles dealt per XCD: blocks b, b+8, b+16, ... (one XCD) take consecutive tiles, so a
 // run's neighbouring reads meet in one L2 (bw_probe: gather 0.49 -> 0.44 ms)
@@ -181,7 +193,7 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
     if (T >= ntp) return;
     __shared__ GsSmem sm;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t cur = st->cur;
+    const uint32_t cur = gs_cur(st, pass);
     const uint32_t *src = cur == 0 ? in : cur == 1 ? bufA : bufB;
     uint32_t *dst = cur == 1 ? bufB : bufA;
     const uint32_t L0 = T * (uint32_t)GT;
@@ -378,11 +390,7 @@ __global__ __launch_bounds__(1024) void k_gscan(const uint32_t *__restrict__ gsu
         run += v[i];
     }
     if (tid == 1023) tot[d] = run;
-    if (d == 0 && tid == 0) {
-        const uint32_t nxt = st->cur == 1 ? 2u : 1u;
-        (nxt == 1 ? tA : tB).ls[(size_t)256 * ntp] = n;  // sentinel start after the last run
-        st->cur = nxt;
-    }
+    if (d == 0 && tid == 0) (gs_dst(st, pass) == 1u ? tA : tB).ls[(size_t)256 * ntp] = n;  // after the last run
     if (d == 0 && pass == 0 && tid < 4u) {
         uint32_t mn = 255u, mx = 0u;
         for (uint32_t g = 0; g < ngroups; ++g) {
@@ -394,17 +402,23 @@ __global__ __launch_bounds__(1024) void k_gscan(const uint32_t *__restrict__ gsu
     }
 }
 
-// k_gout: the tables of this pass's output buffer (now st->cur), GS_GROUP tiles per
-// workgroup (4 threads per digit, 16 tiles each); digit-major writes go through LDS so
-// each is a 256-B line segment.
+// k_gout: the tables of this pass's output buffer, GS_GROUP tiles per workgroup (4
+// threads per digit, 16 tiles each); digit-major writes go through LDS so each is a
+// 256-B line segment.  SMALL (at most GS_SMALL_NG groups): the workgroup sums the
+// earlier groups' and all groups' counts itself from the tile rows, so k_gsum and
+// k_gscan are not launched (the scan is one launch instead of three; at 2^20 keys the
+// launches, not the bytes, set the time); workgroup 0 also does k_gscan's chores.
+template <bool SMALL>
 __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, const uint32_t *__restrict__ gsx,
-                                               const uint32_t *__restrict__ tot, GsTables tA, GsTables tB,
-                                               const GsState *st, int pass, uint32_t ntp, uint32_t n) {
+                                               const uint32_t *__restrict__ tot, const uint32_t *__restrict__ mm,
+                                               GsTables tA, GsTables tB, GsState *st, int pass, uint32_t ntp,
+                                               uint32_t n) {
     if (!gs_active(st, pass)) return;
     __shared__ uint32_t lsb[GS_GROUP][257], srb[GS_GROUP][257];
     __shared__ uint32_t part[4][256];
+    __shared__ uint32_t pre[2][4][256];
     __shared__ uint32_t wsum[16];
-    const GsTables tb = st->cur == 1 ? tA : tB;
+    const GsTables tb = gs_dst(st, pass) == 1u ? tA : tB;
     const uint32_t g = blockIdx.x, tid = threadIdx.x, d = tid & 255u, q = tid >> 8;
     constexpr int TPQ = GS_GROUP / 4;
     const uint32_t t0 = g * GS_GROUP + q * TPQ;
@@ -415,12 +429,45 @@ __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, 
         h += w[i] >> 16;
     }
     part[q][d] = h;
+    uint32_t total = 0, before = 0;
+    if constexpr (SMALL) {
+        // counts of digit d in the tiles before this group and in all tiles
+        uint32_t sb = 0, sa = 0;
+#pragma unroll 8
+        for (uint32_t t = q; t < ntp; t += 4u) {
+            const uint32_t c = rt[(size_t)t * 256 + d] >> 16;
+            sa += c;
+            sb += t < g * (uint32_t)GS_GROUP ? c : 0u;
+        }
+        pre[0][q][d] = sb;
+        pre[1][q][d] = sa;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            before += pre[0][r][d];
+            total += pre[1][r][d];
+        }
+        if (g == 0 && tid == 0) tb.ls[(size_t)256 * ntp] = n;  // sentinel start after the last run
+        if (g == 0 && pass == 0 && tid < 4u) {
+            uint32_t mn = 255u, mx = 0u;
+            for (uint32_t t = 0; t < ntp; ++t) {
+                const uint32_t a = (mm[2 * t] >> (8 * tid)) & 255u, b = (mm[2 * t + 1] >> (8 * tid)) & 255u;
+                mn = a < mn ? a : mn;
+                mx = b > mx ? b : mx;
+            }
+            st->dmin[tid] = mn;
+            st->dmax[tid] = mx;
+        }
+    } else {
+        total = tot[d];
+        before = gsx[(size_t)g * 256 + d];
+    }
     // global exclusive digit offsets from the digit totals
-    const uint32_t gx = block_excl_scan<1024, 256>(q == 0 ? tot[d] : 0u, wsum);
+    const uint32_t gx = block_excl_scan<1024, 256>(q == 0 ? total : 0u, wsum);
     __shared__ uint32_t gxs[256];
     if (q == 0) gxs[d] = gx;
     __syncthreads();
-    uint32_t run = gxs[d] + gsx[(size_t)g * 256 + d];
+    uint32_t run = gxs[d] + before;
     for (uint32_t r = 0; r < q; ++r) run += part[r][d];
 #pragma unroll
     for (int i = 0; i < TPQ; ++i) {
@@ -454,7 +501,7 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gcopy(const uint32_t *_
     if (T >= ntp) return;
     __shared__ GsRuns g;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t cur = st->cur;
+    const uint32_t cur = gs_cur(st, 4);
     const uint32_t L0 = T * (uint32_t)GT;
     const uint32_t nvalid = (n - L0) < (uint32_t)GT ? (n - L0) : (uint32_t)GT;
     uint32_t k[GK];
@@ -526,9 +573,13 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
         k_gsweep<<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, mm, st, p, (uint32_t)n, ntp, flip);
         if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        k_gsum<<<ng, 256, 0, s>>>(rt, mm, gsum, gmm, st, p, ntp);
-        k_gscan<<<256, 1024, 0, s>>>(gsum, gsx, gx, gmm, st, p, ng, (uint32_t)n, ntp, t[0], t[1]);
-        k_gout<<<ng, 1024, 0, s>>>(rt, gsx, gx, t[0], t[1], st, p, ntp, (uint32_t)n);
+        if (ng <= (uint32_t)GS_SMALL_NG) {
+            k_gout<true><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, t[0], t[1], st, p, ntp, (uint32_t)n);
+        } else {
+            k_gsum<<<ng, 256, 0, s>>>(rt, mm, gsum, gmm, st, p, ntp);
+            k_gscan<<<256, 1024, 0, s>>>(gsum, gsx, gx, gmm, st, p, ng, (uint32_t)n, ntp, t[0], t[1]);
+            k_gout<false><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, t[0], t[1], st, p, ntp, (uint32_t)n);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GCOPY, s);
