@@ -11,9 +11,15 @@ so every step sorts the same input.
 
 N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): the
 merge-sort path of the north_star.  Each rank holds a fixed 2^log2n-key shard
-(weak scaling), sorts it locally with the radix kernels, then the pairwise
-merge-split network exchanges keys over RCCL send/recv (dist.py).  value = all
-ranks' keys / max-over-ranks time.
+(weak scaling), sorts it locally with the radix kernels, then the splitter
+exchange (or, --exchange pairwise, the bitonic merge-split network) moves keys
+over RCCL send/recv (dist.py).  value = all ranks' keys / max-over-ranks time.
+
+host_path (after the timed region, rank 0, in a child process): the reference's
+own calling convention -- a pageable host int* of 2^30 keys (BASELINE config 5)
+sorted in place, PCIe copies included: labsort_sort_host on one GPU, and at N > 1
+labsort_sort_host_multi over devices 0..N-1 (per-GPU PCIe shards + RCCL exchange).
+Reported beside the headline, never as `value`.
 
 After the timed region the output is verified with size-independent properties
 (no descents, same sum / sum of squares / digit histograms as the input);
@@ -59,6 +65,9 @@ def parse():
                     help="N>1: all-peer splitter exchange + merge tree, or the bitonic pairwise merge-split network")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 only; gloo (+ host-staged exchange) is a test mode for several ranks on one GPU")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the host-pointer (PCIe-inclusive) leg")
+    ap.add_argument("--host-log2n", type=int, default=30, help="host-pointer leg: keys = 2^host-log2n")
+    ap.add_argument("--host-leg", action="store_true", help=argparse.SUPPRESS)  # the child process of host_path
     return ap.parse_args()
 
 
@@ -162,8 +171,90 @@ def cpu_baseline(budget_s: float, n: int, ls):
                                       f"{treps} x 2^24 keys, {tt:.1f} s"}}
 
 
+def host_fingerprint(np, a):
+    """count, sum and sum of squares (mod 2^64) of the keys as uint32, in 64 Mi-key chunks"""
+    u = a.view(np.uint32)
+    s1 = s2 = 0
+    for i in range(0, u.size, 1 << 26):
+        c = u[i:i + (1 << 26)].astype(np.uint64)
+        s1 = (s1 + int(c.sum(dtype=np.uint64))) & (2**64 - 1)
+        s2 = (s2 + int((c * c).sum(dtype=np.uint64))) & (2**64 - 1)
+    return u.size, s1, s2
+
+
+def host_sorted(np, a) -> bool:
+    v = a  # int32: order_array's signed order
+    for i in range(0, v.size - 1, 1 << 26):
+        c = v[i:i + (1 << 26) + 1]
+        if not bool((c[1:] >= c[:-1]).all()):
+            return False
+    return True
+
+
+def host_leg_main(args) -> None:
+    """Child process of the host_path leg: one pageable int32 host array sorted in place
+    through labsort_sort_host (1 GPU) and labsort_sort_host_multi (devices 0..N-1)."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, REPO)
+    ls = importlib.import_module(PKG_NAME)
+    n = 1 << args.host_log2n
+    t = torch.empty(n, dtype=torch.int32, device="cuda:0")
+    ls.fill(t, n, SEED + 5, "u31")  # the reference's keys: non-negative int (main.cpp rand())
+    torch.cuda.synchronize()
+    src = t.cpu().numpy()
+    del t
+    torch.cuda.empty_cache()
+    fp = host_fingerprint(np, src)
+    work = np.empty_like(src)
+    out = {"n": n, "key": "i32 (order_array)", "input": "pageable host array, u31 keys (main.cpp's rand())",
+           "note": "PCIe-inclusive: H2D + sort + D2H of a host int*, in place (never `value`)"}
+
+    def timed(fn, reps):
+        ts = []
+        for _ in range(reps):
+            np.copyto(work, src)
+            t0 = time.perf_counter()
+            fn(work)
+            ts.append(time.perf_counter() - t0)
+        ok = host_sorted(np, work) and host_fingerprint(np, work) == fp
+        return sorted(ts)[len(ts) // 2], ok
+
+    el, ok = timed(lambda a: ls.sort_host(a, algo="auto"), 3)
+    out["single_gpu"] = {"ms": round(el * 1e3, 3), "Mkeys_s": round(n / el / 1e6, 2), "verified": ok,
+                         "call": "labsort_sort_host (order_array)"}
+    if args.gpus > 1:
+        el, ok = timed(lambda a: ls.sort_host_multi(a, args.gpus), 3)
+        ph, sent = ls.multi_timing()
+        out["multi_gpu"] = {"n_gpus": args.gpus, "ms": round(el * 1e3, 3), "Mkeys_s": round(n / el / 1e6, 2),
+                            "verified": ok, "call": "labsort_sort_host_multi (LABSORT_GPUS=N order_array)",
+                            "phases_ms": {k: round(v, 3) for k, v in ph.items()}, "max_sent_bytes": sent}
+    print(json.dumps(out), flush=True)
+
+
+def host_leg(args, timeout_s: int = 240):
+    """Run the host_path leg in a child process: it opens every GPU it uses itself, and a
+    hang or fault there ends only the child (reported as an error)."""
+    import subprocess
+    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+            "ROLE_RANK", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    cmd = [sys.executable, os.path.abspath(__file__), "--host-leg", "--gpus", str(args.gpus),
+           "--host-log2n", str(args.host_log2n)]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout_s} s"}
+    for ln in reversed(r.stdout.splitlines()):
+        if ln.startswith("{"):
+            return json.loads(ln)
+    return {"error": f"exit {r.returncode}: {r.stderr.strip()[-400:]}"}
+
+
 def main():
     args = parse()
+    if args.host_leg:
+        return host_leg_main(args)
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -415,6 +506,13 @@ def main():
                 "note": "max over ranks; exchange time is host wall time around the point-to-point calls "
                         "(stream synchronised on both sides)"}
 
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+    # the host-pointer leg runs once every rank is done with its GPU
+    hostp = host_leg(args) if rank == 0 and not args.no_host_path and args.backend == "nccl" else None
+
     if rank == 0:
         avg_ms = k_ms / k_cnt if k_cnt else None
         per_launch_bytes = 16.0 * n if args.algo == "pairs" else 8.0 * n  # key (+ payload) read + written
@@ -462,10 +560,9 @@ def main():
         if xgmi:
             line["config"]["local_algo"] = "radix"
             line["xgmi"] = xgmi
+        if hostp:
+            line["host_path"] = hostp
         print(json.dumps(line), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

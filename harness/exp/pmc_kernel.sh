@@ -11,7 +11,7 @@ SETS=("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST
 i=0
 for set in "${SETS[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "$KRE" --output-format csv -d "$O/pmc_${TAG}_$i" -o run -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$O/pmc_${TAG}_$i.log" 2>&1 || { echo "pass $i failed"; tail -20 "$O/pmc_${TAG}_$i.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "$KRE" --output-format csv -d "$O/pmc_${TAG}_$i" -o run -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-host-path ${BENCH_ARGS:-} > "$O/pmc_${TAG}_$i.log" 2>&1 || { echo "pass $i failed"; tail -20 "$O/pmc_${TAG}_$i.log"; exit 1; }
 done
 python3 - "$O" "$TAG" <<'PY' | tee "$O/pmc_$2.txt"
 import csv, sys, glob, collections

@@ -13,9 +13,9 @@ fi
 for lib in $P ${LIBS-harness/exp/liblabsort_stamps_x0.so}; do
   for seg in ${SEGS:-first on}; do
     echo "== $lib SEG=$seg"
-    LABSORT_SEG=$seg LABSORT_LIBRARY="$R/$lib" timeout -k 10 200 python "$R/bench.py" --no-cpu-baseline > "$O/xe.json" 2> "$O/xe.err" || { tail -5 "$O/xe.err"; exit 1; }
+    LABSORT_SEG=$seg LABSORT_LIBRARY="$R/$lib" timeout -k 10 200 python "$R/bench.py" --no-cpu-baseline --no-host-path > "$O/xe.json" 2> "$O/xe.err" || { tail -5 "$O/xe.err"; exit 1; }
     grep -o '"ms_per_step": [0-9.]*\|avg_launch_ms": [0-9.]*' "$O/xe.json" | tr '\n' ' '; echo
-    LABSORT_SEG=$seg LABSORT_LIBRARY="$R/$lib" timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$O/xe_prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$O/xe_prof.log" 2>&1 || { tail -5 "$O/xe_prof.log"; exit 1; }
+    LABSORT_SEG=$seg LABSORT_LIBRARY="$R/$lib" timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$O/xe_prof" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > "$O/xe_prof.log" 2>&1 || { tail -5 "$O/xe_prof.log"; exit 1; }
     python3 "$R/harness/exp/pass_times.py" "$O/xe_prof/run_kernel_trace.csv"
     rm -rf "$O/xe_prof"
   done

@@ -26,10 +26,10 @@ if [[ "$STEPS" == all || "$STEPS" == *bench* ]]; then
 fi
 if [[ "$STEPS" == all || "$STEPS" == *prof* ]]; then
   run rocprof stats
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline > "$O/prof_$TAG.log" 2>&1 || { tail -30 "$O/prof_$TAG.log"; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof_$TAG" -o run -- python3 "$R/bench.py" --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > "$O/prof_$TAG.log" 2>&1 || { tail -30 "$O/prof_$TAG.log"; exit 1; }
   for c in FETCH_SIZE WRITE_SIZE; do
     run rocprof pmc $c
-    timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${c}_$TAG" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline > "$O/pmc_${c}_$TAG.log" 2>&1 || { tail -30 "$O/pmc_${c}_$TAG.log"; exit 1; }
+    timeout -k 10 400 rocprofv3 --pmc $c --output-format csv -d "$O/pmc_${c}_$TAG" -o run -- python3 "$R/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-host-path > "$O/pmc_${c}_$TAG.log" 2>&1 || { tail -30 "$O/pmc_${c}_$TAG.log"; exit 1; }
   done
 fi
 run done
@@ -42,5 +42,5 @@ if [[ "$STEPS" == *dist* ]]; then
 fi
 if [[ "$STEPS" == *mprof* ]]; then
   run rocprof stats merge
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/mprof_$TAG" -o run -- python3 "$R/bench.py" --algo merge --steps 10 --warmup 2 --no-cpu-baseline > "$O/mprof_$TAG.log" 2>&1 || { tail -30 "$O/mprof_$TAG.log"; exit 1; }
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/mprof_$TAG" -o run -- python3 "$R/bench.py" --algo merge --steps 10 --warmup 2 --no-cpu-baseline --no-host-path > "$O/mprof_$TAG.log" 2>&1 || { tail -30 "$O/mprof_$TAG.log"; exit 1; }
 fi

@@ -13,7 +13,7 @@ fi
 rm -rf "$O"/pmc_os_*
 for set in "${SETS[@]}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "${KRE:-onesweep_p}" --output-format csv -d "$O/pmc_os_$i" -o run -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} > "$O/pmc_os_$i.log" 2>&1 || { echo "pass $i failed"; tail -20 "$O/pmc_os_$i.log"; exit 1; }
+  timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "${KRE:-onesweep_p}" --output-format csv -d "$O/pmc_os_$i" -o run -- python3 "$R/bench.py" --steps 1 --warmup 1 --no-cpu-baseline --no-host-path ${BENCH_ARGS:-} > "$O/pmc_os_$i.log" 2>&1 || { echo "pass $i failed"; tail -20 "$O/pmc_os_$i.log"; exit 1; }
 done
 python3 - "$O" <<'PY'
 import csv, sys, glob, collections

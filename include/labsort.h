@@ -47,8 +47,10 @@ extern "C" {
 #define LABSORT_ALGO_MERGE 1     /* LDS tile radix + merge-path merge passes */
 #define LABSORT_ALGO_RADIX1 2    /* LSD radix with 1-bit digits: letra.pdf's split, 32 passes */
 #define LABSORT_ALGO_AUTO 3      /* MERGE for n <= LABSORT_AUTO_MERGE_MAX_KEYS (fewer launches and
-                                    less fixed cost at small n), RADIX above; the default of the
-                                    host drop-ins order_array / sort (LABSORT_ALGO env overrides) */
+                                    less fixed cost at small n) and above the radix limit
+                                    (labsort_max_keys(RADIX), e.g. 2^30 keys), RADIX between; the
+                                    default of the host drop-ins order_array / sort (LABSORT_ALGO
+                                    env overrides) */
 #define LABSORT_AUTO_MERGE_MAX_KEYS (1u << 20)
 
 /* key types: how the 32-bit words are ordered */

@@ -278,12 +278,25 @@ int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char 
 // ---------------------------------------------------------------------------------
 // host-pointer API state: one cached device buffer + workspace per device
 // ---------------------------------------------------------------------------------
+// Host-pointer pipeline (labsort_sort_host, n >= HOST_PIPE_MIN): HOST_CHUNKS chunks
+// copied H2D on `copy` while `stream` sorts the chunks that have landed; the chunk
+// runs are merged in two halves (labsort_merge_runs), then the final merge of the
+// halves runs as HOST_RANGES diagonal ranges whose D2H copies start as each lands.
+constexpr int HOST_CHUNKS = 8, HOST_RANGES = 8;
+constexpr size_t HOST_PIPE_MIN = (size_t)1 << 27;  // r19: 2^26 0.3 ms slower, 2^27 even, 2^28 0.7 ms
+                                                    // faster, 2^30 187 -> 157 ms (PCIe-bound)
+
 struct DeviceCache {
     void *keys = nullptr;
     size_t keys_bytes = 0;
     void *ws = nullptr;
     size_t ws_bytes = 0;
     hipStream_t stream = nullptr;
+    // pipeline only
+    void *keys2 = nullptr, *mws = nullptr, *part = nullptr, *errs = nullptr;
+    size_t keys2_bytes = 0, mws_bytes = 0, part_bytes = 0, errs_bytes = 0;
+    hipStream_t copy = nullptr;
+    hipEvent_t ev[HOST_CHUNKS + HOST_RANGES] = {};
 };
 std::mutex g_host_mu;
 std::vector<DeviceCache> g_cache;
@@ -322,7 +335,8 @@ int multi_gpus() {
 // 0.134 / 0.220 / 0.286 ms at 2^16 / 2^20 / 2^22; equal at 2^23; radix faster above.
 int resolve_algo(int algo, size_t n) {
     if (algo != LABSORT_ALGO_AUTO) return algo;
-    return n <= (size_t)LABSORT_AUTO_MERGE_MAX_KEYS ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
+    // merge for small arrays (fewer launches) and past the radix limit (2^30 - 1 keys)
+    return n <= (size_t)LABSORT_AUTO_MERGE_MAX_KEYS || n > RADIX_MAX_N ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
 }
 
 }  // namespace
@@ -391,7 +405,7 @@ int labsort_last_hip_error(void) { return g_last_hip; }
 const char *labsort_hip_error_string(int e) { return hipGetErrorString((hipError_t)e); }
 
 size_t labsort_max_keys(int algo) {
-    if (algo == LABSORT_ALGO_MERGE) return (size_t)0x7FFFFFFFu;
+    if (algo == LABSORT_ALGO_MERGE || algo == LABSORT_ALGO_AUTO) return (size_t)0x7FFFFFFFu;
     return RADIX_MAX_N;
 }
 size_t labsort_tile_keys(void) { return (size_t)TS_TILE; }
@@ -464,14 +478,110 @@ int labsort_workspace_status(const void *d_ws, size_t n, int algo, void *stream)
 }
 
 int labsort_pairs_workspace_status(const void *d_ws, size_t n, int algo, void *stream) {
-    if (algo == LABSORT_ALGO_AUTO) algo = n <= (size_t)LABSORT_AUTO_MERGE_MAX_KEYS ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
+    algo = resolve_algo(algo, n);
     return read_status(d_ws, n > (size_t)TS_TILE_KV && algo == LABSORT_ALGO_RADIX, as_stream(stream));
 }
+
+namespace {
+// LABSORT_HOST_PIPE: "0" never, "1" from 2^16 keys (tests), unset from HOST_PIPE_MIN
+bool host_pipe_enabled(size_t n, int algo) {
+    if (algo == LABSORT_ALGO_RADIX1) return false;
+    const char *e = std::getenv("LABSORT_HOST_PIPE");
+    if (e && !std::strcmp(e, "0")) return false;
+    return n >= (e && !std::strcmp(e, "1") ? (size_t)1 << 16 : HOST_PIPE_MIN);
+}
+
+// The pipelined host sort (see HOST_CHUNKS).  Chunk i: H2D into X on c.copy (a pageable
+// copy returns once staged, so the host issues chunk i+1's copy while the GPU sorts
+// chunk i), then sorted X -> Y on c.stream; its device error word is copied aside.
+// Halves: Y's 4 + 4 chunk runs merged into X (the left half while the right half
+// is still being copied).  Final: merge(X left, X right) -> Y by
+// ranges, each range's D2H on c.copy after its merge.
+int sort_host_pipelined(DeviceCache &c, void *h_keys, size_t n, int key_type, int algo) {
+    const size_t m = (n + HOST_CHUNKS - 1) / HOST_CHUNKS;  // chunk keys (last one ragged)
+    const int calgo = resolve_algo(algo, m);
+    const size_t half = m * (HOST_CHUNKS / 2);
+    int st;
+    if ((st = ensure_buffer(&c.keys, &c.keys_bytes, n * 4))) return st;
+    if ((st = ensure_buffer(&c.keys2, &c.keys2_bytes, n * 4))) return st;
+    if ((st = ensure_buffer(&c.ws, &c.ws_bytes, labsort_workspace_bytes(m, calgo)))) return st;
+    const size_t mwb = labsort_merge_runs_workspace_bytes(half > n - half ? half : n - half);
+    if ((st = ensure_buffer(&c.mws, &c.mws_bytes, mwb))) return st;
+    if ((st = ensure_buffer(&c.part, &c.part_bytes, labsort_merge_parts((n + HOST_RANGES - 1) / HOST_RANGES) * 4)))
+        return st;
+    if ((st = ensure_buffer(&c.errs, &c.errs_bytes, HOST_CHUNKS * 4))) return st;
+    if (!c.copy) HIP_TRY(hipStreamCreateWithFlags(&c.copy, hipStreamNonBlocking));
+    for (auto &e : c.ev)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    uint32_t *h = static_cast<uint32_t *>(h_keys);
+    uint32_t *X = static_cast<uint32_t *>(c.keys), *Y = static_cast<uint32_t *>(c.keys2);
+    uint32_t *errs = static_cast<uint32_t *>(c.errs);
+    // the previous call's D2H copies of Y have finished (c.copy), before Y is written
+    HIP_TRY(hipEventRecord(c.ev[0], c.copy));
+    HIP_TRY(hipStreamWaitEvent(c.stream, c.ev[0], 0));
+    HIP_TRY(launch_zero(errs, HOST_CHUNKS * 4, c.stream));
+    HIP_TRY(hipEventRecord(c.ev[1], c.stream));
+    HIP_TRY(hipStreamWaitEvent(c.copy, c.ev[1], 0));
+    // the two halves of HOST_CHUNKS / 2 chunk runs each, Y -> X: the left half is merged
+    // while the right half's chunks are still being copied
+    auto merge_half = [&](int hf) -> int {
+        const size_t b = hf ? half : 0, e = hf ? n : (half < n ? half : n);
+        if (e <= b) return LABSORT_OK;
+        size_t off[HOST_CHUNKS / 2 + 1];
+        int nr = 0;
+        for (int q = 0; q < HOST_CHUNKS / 2; ++q) {
+            const size_t o = b + (size_t)q * m;
+            if (o >= e) break;
+            off[nr++] = o - b;
+        }
+        off[nr] = e - b;
+        return labsort_merge_runs(Y + b, X + b, off, nr, key_type, c.mws, c.mws_bytes, c.stream);
+    };
+    for (int i = 0; i < HOST_CHUNKS; ++i) {
+        const size_t o = (size_t)i * m, len = o < n ? (n - o < m ? n - o : m) : 0;
+        if (len) {
+            HIP_TRY(hipMemcpyAsync(X + o, h + o, len * 4, hipMemcpyHostToDevice, c.copy));
+            HIP_TRY(hipEventRecord(c.ev[i], c.copy));
+            HIP_TRY(hipStreamWaitEvent(c.stream, c.ev[i], 0));
+            if ((st = labsort_sort_device(X + o, Y + o, len, key_type, calgo, c.ws, c.ws_bytes, c.stream))) return st;
+            if (!small_path(len, calgo) && calgo != LABSORT_ALGO_MERGE)  // the radix layout's error word
+                HIP_TRY(hipMemcpyAsync(errs + i, c.ws, 4, hipMemcpyDeviceToDevice, c.stream));
+        }
+        if (i == HOST_CHUNKS / 2 - 1 && (st = merge_half(0))) return st;
+    }
+    if ((st = merge_half(1))) return st;
+    // final merge X[0, half) with X[half, n) into Y by ranges; D2H as each lands
+    const size_t la = half < n ? half : n, lb = n - la, rl = (n + HOST_RANGES - 1) / HOST_RANGES;
+    for (int r = 0; r < HOST_RANGES; ++r) {
+        const size_t d0 = (size_t)r * rl, d1 = d0 + rl < n ? d0 + rl : n;
+        if (d0 >= d1) break;
+        if ((st = labsort_merge(X, la, X + la, lb, Y + d0, d0, d1, key_type, static_cast<uint32_t *>(c.part),
+                                c.stream)))
+            return st;
+        HIP_TRY(hipEventRecord(c.ev[HOST_CHUNKS + r], c.stream));
+    }
+    for (int r = 0; r < HOST_RANGES; ++r) {
+        const size_t d0 = (size_t)r * rl, d1 = d0 + rl < n ? d0 + rl : n;
+        if (d0 >= d1) break;
+        HIP_TRY(hipStreamWaitEvent(c.copy, c.ev[HOST_CHUNKS + r], 0));
+        HIP_TRY(hipMemcpyAsync(h + d0, Y + d0, (d1 - d0) * 4, hipMemcpyDeviceToHost, c.copy));
+    }
+    HIP_TRY(hipStreamSynchronize(c.copy));
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    uint32_t herr[HOST_CHUNKS];
+    HIP_TRY(hipMemcpy(herr, errs, sizeof herr, hipMemcpyDeviceToHost));
+    for (int i = 0; i < HOST_CHUNKS; ++i)
+        if (herr[i]) return LABSORT_ERR_DEVICE;
+    return LABSORT_OK;
+}
+}  // namespace
 
 int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo) {
     if (n == 0) return LABSORT_OK;
     if (!h_keys) return LABSORT_ERR_ARG;
     if (n > labsort_max_keys(algo)) return LABSORT_ERR_ARG;
+    if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
+    const int requested = algo;  // AUTO is resolved again per chunk by the pipeline
     algo = resolve_algo(algo, n);
     std::lock_guard<std::mutex> lk(g_host_mu);
     int dev = 0;
@@ -479,6 +589,7 @@ int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo) {
     if ((int)g_cache.size() <= dev) g_cache.resize(dev + 1);
     DeviceCache &c = g_cache[dev];
     if (!c.stream) HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+    if (host_pipe_enabled(n, algo)) return sort_host_pipelined(c, h_keys, n, key_type, requested);
     int st = ensure_buffer(&c.keys, &c.keys_bytes, n * 4);
     if (st) return st;
     const size_t wsb = labsort_workspace_bytes(n, algo);
@@ -651,7 +762,7 @@ int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void
     if (!d_keys_in || !d_vals_in || !d_keys_out || !d_vals_out) return LABSORT_ERR_ARG;
     if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
     if (algo != LABSORT_ALGO_RADIX && algo != LABSORT_ALGO_MERGE && algo != LABSORT_ALGO_AUTO) return LABSORT_ERR_ARG;
-    if (algo == LABSORT_ALGO_AUTO) algo = n <= (size_t)LABSORT_AUTO_MERGE_MAX_KEYS ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
+    algo = resolve_algo(algo, n);
     if (n > (algo == LABSORT_ALGO_MERGE ? (size_t)0x7FFFFFFFu : RADIX_MAX_N)) return LABSORT_ERR_ARG;
     // in place only as a whole: one side aliased and the other not would read
     // payloads that the key side's passes already overwrote

@@ -12,7 +12,7 @@
 //     output, sorted by digit p in LDS (stable wave rank, as the onesweep pass), and
 //     written back CONTIGUOUSLY at T's own position: whole lines, no partial granules.
 //     The tile's digit counts and local offsets go to a row of `rt`.
-//   scan (k_gsum, k_gtop, k_gout): from the rows, the logical start of every
+//   scan (k_gsum, k_gout): from the rows, the logical start of every
 //     (tile, digit) run (global digit offset + counts of earlier tiles) in digit-major
 //     order, its source address, and for every next-pass tile the first run it covers.
 //     This is the global exclusive scan of letra.pdf's split (lab.cu's per-bit
@@ -23,7 +23,8 @@
 // Pass 0 reads the input contiguously and also records every tile's digit min/max, so
 // passes whose digit is the same for every key are skipped on the device (the
 // deterministic counterpart of the reference's "stop when sorted", lab.cu:61).
-// No decoupled look-back, no spin: tiles of a pass are independent.
+// Tiles of a pass are independent; the only look-back is k_gsum's over the groups of
+// GS_GROUP tiles (at most 128 of them), and only above GS_SMALL_NG groups.
 //
 // Logical input of pass p >= 1 (previous pass q wrote buffer X): run (t, d) = the keys
 // of digit d in tile t of X, at X[t*TILE + lo(t,d)], length h(t,d); runs in the order
@@ -52,11 +53,13 @@ struct GsTables {
 
 // Workspace header (first 512 B; word 0 is the labsort error word, never set here)
 struct GsState {
-    uint32_t err;
+    uint32_t err;       // labsort's device error word (a scan look-back spin expired)
     uint32_t pad;
     uint32_t dmin[4];   // per digit, min / max over all keys (flipped digit values), from pass 0
     uint32_t dmax[4];
+    uint32_t gctr[4];   // per pass: scan groups acquired (k_gsum's dynamic group ids)
 };
+constexpr uint32_t GS_SPIN_LIMIT = 1u << 22;
 
 __device__ __forceinline__ bool gs_active(const GsState *st, int pass) {
     return pass == 0 || st->dmin[pass] != st->dmax[pass];
@@ -340,18 +343,48 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
 }
 
 // ---- scan of the tile rows ------------------------------------------------------------
-// k_gsum: column sums of GS_GROUP consecutive tiles' counts (and, after pass 0, their
-// digit min / max).
+// k_gsum: column sums of GS_GROUP consecutive tiles' counts, and their exclusive prefix
+// over the groups by decoupled look-back (groups taken in order from a counter, so a
+// group only waits on groups already running; every wait bounded: an expired spin sets
+// the error word that labsort_workspace_status reports).  The last group writes the
+// digit totals.  After pass 0 it also reduces its tiles' digit min / max.
 __global__ __launch_bounds__(256) void k_gsum(const uint32_t *__restrict__ rt, const uint32_t *__restrict__ mm,
-                                              uint32_t *__restrict__ gsum, uint32_t *__restrict__ gmm,
-                                              const GsState *st, int pass, uint32_t ntp) {
+                                              uint32_t *__restrict__ gsx, uint32_t *__restrict__ tot,
+                                              uint32_t *__restrict__ gmm, uint32_t *flags, GsState *st, int pass,
+                                              uint32_t ntp, uint32_t ngroups) {
     if (!gs_active(st, pass)) return;
-    const uint32_t g = blockIdx.x, d = threadIdx.x;
+    __shared__ uint32_t gid;
+    const uint32_t d = threadIdx.x;
+    if (d == 0) gid = atomicAdd(&st->gctr[pass], 1u);
+    __syncthreads();
+    const uint32_t g = gid;
     const uint32_t t0 = g * GS_GROUP, t1 = t0 + GS_GROUP < ntp ? t0 + GS_GROUP : ntp;
     uint32_t h = 0;
 #pragma unroll 8
     for (uint32_t t = t0; t < t1; ++t) h += rt[(size_t)t * 256 + d] >> 16;
-    gsum[(size_t)g * 256 + d] = h;
+    uint32_t *fl = flags + (size_t)pass * ngroups * 256;
+    st_agent(fl + (size_t)g * 256 + d, (g == 0 ? LB_INC : LB_AGG) | h);
+    uint32_t excl = 0;
+    if (g > 0) {
+        uint32_t t = g - 1, spins = 0;
+        for (;;) {
+            const uint32_t w = ld_agent(fl + (size_t)t * 256 + d);
+            if ((w & ~LB_VAL) == 0u) {
+                if (++spins > GS_SPIN_LIMIT) {
+                    atomicOr(&st->err, 1u);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += w & LB_VAL;
+            if (w & LB_INC) break;
+            --t;
+        }
+        st_agent(fl + (size_t)g * 256 + d, LB_INC | (excl + h));
+    }
+    gsx[(size_t)g * 256 + d] = excl;
+    if (g + 1 == ngroups) tot[d] = excl + h;
     if (pass == 0 && d < 4u) {
         uint32_t mn = 255u, mx = 0u;
         for (uint32_t t = t0; t < t1; ++t) {
@@ -364,53 +397,17 @@ __global__ __launch_bounds__(256) void k_gsum(const uint32_t *__restrict__ rt, c
     }
 }
 
-// k_gscan (one workgroup per digit d): exclusive scan of digit d's group sums over the
-// groups, and d's total; workgroup 0 then moves the current logical order to this
-// pass's output buffer and, after pass 0, reduces the digit min / max.
-__global__ __launch_bounds__(1024) void k_gscan(const uint32_t *__restrict__ gsum, uint32_t *__restrict__ gsx,
-                                                uint32_t *__restrict__ tot, const uint32_t *__restrict__ gmm,
-                                                GsState *st, int pass, uint32_t ngroups, uint32_t n, uint32_t ntp,
-                                                GsTables tA, GsTables tB) {
-    if (!gs_active(st, pass)) return;
-    __shared__ uint32_t wsum[16];
-    const uint32_t tid = threadIdx.x, d = blockIdx.x;
-    constexpr int GPT = 4;  // groups per thread: ngroups <= 4096 (2^35 keys)
-    uint32_t v[GPT], s = 0;
-#pragma unroll
-    for (int i = 0; i < GPT; ++i) {
-        const uint32_t g = tid * GPT + i;
-        v[i] = g < ngroups ? gsum[(size_t)g * 256 + d] : 0u;
-        s += v[i];
-    }
-    uint32_t run = block_excl_scan<1024, 1024>(s, wsum);
-#pragma unroll
-    for (int i = 0; i < GPT; ++i) {
-        const uint32_t g = tid * GPT + i;
-        if (g < ngroups) gsx[(size_t)g * 256 + d] = run;
-        run += v[i];
-    }
-    if (tid == 1023) tot[d] = run;
-    if (d == 0 && tid == 0) (gs_dst(st, pass) == 1u ? tA : tB).ls[(size_t)256 * ntp] = n;  // after the last run
-    if (d == 0 && pass == 0 && tid < 4u) {
-        uint32_t mn = 255u, mx = 0u;
-        for (uint32_t g = 0; g < ngroups; ++g) {
-            mn = gmm[g * 8 + tid] < mn ? gmm[g * 8 + tid] : mn;
-            mx = gmm[g * 8 + 4 + tid] > mx ? gmm[g * 8 + 4 + tid] : mx;
-        }
-        st->dmin[tid] = mn;
-        st->dmax[tid] = mx;
-    }
-}
-
 // k_gout: the tables of this pass's output buffer, GS_GROUP tiles per workgroup (4
 // threads per digit, 16 tiles each); digit-major writes go through LDS so each is a
 // 256-B line segment.  SMALL (at most GS_SMALL_NG groups): the workgroup sums the
-// earlier groups' and all groups' counts itself from the tile rows, so k_gsum and
-// k_gscan are not launched (the scan is one launch instead of three; at 2^20 keys the
-// launches, not the bytes, set the time); workgroup 0 also does k_gscan's chores.
+// earlier groups' and all groups' counts itself from the tile rows, so k_gsum is not
+// launched (the scan is one launch instead of two; at 2^20 keys the launches, not the
+// bytes, set the time).  Workgroup 0 writes the sentinel and, after pass 0, the digit
+// min / max.
 template <bool SMALL>
 __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, const uint32_t *__restrict__ gsx,
                                                const uint32_t *__restrict__ tot, const uint32_t *__restrict__ mm,
+                                               const uint32_t *__restrict__ gmm,
                                                GsTables tA, GsTables tB, GsState *st, int pass, uint32_t ntp,
                                                uint32_t n) {
     if (!gs_active(st, pass)) return;
@@ -461,6 +458,18 @@ __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, 
     } else {
         total = tot[d];
         before = gsx[(size_t)g * 256 + d];
+        if (g == 0 && tid == 0) tb.ls[(size_t)256 * ntp] = n;  // sentinel start after the last run
+        if (g == 0 && pass == 0 && tid < 4u) {
+            uint32_t mn = 255u, mx = 0u;
+            const uint32_t ng = (ntp + GS_GROUP - 1) / GS_GROUP;
+#pragma unroll 8
+            for (uint32_t gg = 0; gg < ng; ++gg) {
+                mn = gmm[gg * 8 + tid] < mn ? gmm[gg * 8 + tid] : mn;
+                mx = gmm[gg * 8 + 4 + tid] > mx ? gmm[gg * 8 + 4 + tid] : mx;
+            }
+            st->dmin[tid] = mn;
+            st->dmax[tid] = mx;
+        }
     }
     // global exclusive digit offsets from the digit totals
     const uint32_t gx = block_excl_scan<1024, 256>(q == 0 ? total : 0u, wsum);
@@ -522,8 +531,8 @@ GsLayout gs_layout(size_t n) {
     GsLayout L{};
     const size_t ntp = (n + GT - 1) / GT, ng = (ntp + GS_GROUP - 1) / GS_GROUP, ne = 256 * ntp;
     size_t o = 0;
-    L.off_state = o;
-    o = al(o + 512);
+    L.off_state = o;  // state, then the scan look-back flags of the 4 passes: zeroed together
+    o = al(o + 512 + 4 * ng * 256 * 4);
     L.off_a = o;
     o = al(o + n * 4);
     L.off_b = o;
@@ -532,8 +541,6 @@ GsLayout gs_layout(size_t n) {
     o = al(o + ne * 4);
     L.off_mm = o;
     o = al(o + ntp * 8);
-    L.off_gsum = o;
-    o = al(o + ng * 256 * 4);
     L.off_gsx = o;
     o = al(o + ng * 256 * 4);
     L.off_gx = o;
@@ -559,13 +566,14 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
     GsState *st = reinterpret_cast<GsState *>(ws + L.off_state);
     uint32_t *A = reinterpret_cast<uint32_t *>(ws + L.off_a), *B = reinterpret_cast<uint32_t *>(ws + L.off_b);
     uint32_t *rt = reinterpret_cast<uint32_t *>(ws + L.off_rt), *mm = reinterpret_cast<uint32_t *>(ws + L.off_mm);
-    uint32_t *gsum = reinterpret_cast<uint32_t *>(ws + L.off_gsum), *gsx = reinterpret_cast<uint32_t *>(ws + L.off_gsx);
+    uint32_t *gsx = reinterpret_cast<uint32_t *>(ws + L.off_gsx);
     uint32_t *gx = reinterpret_cast<uint32_t *>(ws + L.off_gx), *gmm = reinterpret_cast<uint32_t *>(ws + L.off_gmm);
     GsTables t[2];
     for (int i = 0; i < 2; ++i)
         t[i] = GsTables{reinterpret_cast<uint32_t *>(ws + L.off_ls[i]), reinterpret_cast<uint32_t *>(ws + L.off_sr[i]),
                         reinterpret_cast<uint32_t *>(ws + L.off_first[i])};
-    hipError_t e = launch_zero(ws + L.off_state, 512, s);
+    uint32_t *flags = reinterpret_cast<uint32_t *>(ws + L.off_state + 512);
+    hipError_t e = launch_zero(ws + L.off_state, 512 + (ng > (uint32_t)GS_SMALL_NG ? (size_t)4 * ng * 256 * 4 : 0), s);
     if (e != hipSuccess) return e;
     const unsigned grid = 8u * ((ntp + 7u) / 8u);
     for (int p = 0; p < 4; ++p) {
@@ -574,11 +582,10 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
         if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (ng <= (uint32_t)GS_SMALL_NG) {
-            k_gout<true><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, t[0], t[1], st, p, ntp, (uint32_t)n);
+            k_gout<true><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, gmm, t[0], t[1], st, p, ntp, (uint32_t)n);
         } else {
-            k_gsum<<<ng, 256, 0, s>>>(rt, mm, gsum, gmm, st, p, ntp);
-            k_gscan<<<256, 1024, 0, s>>>(gsum, gsx, gx, gmm, st, p, ng, (uint32_t)n, ntp, t[0], t[1]);
-            k_gout<false><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, t[0], t[1], st, p, ntp, (uint32_t)n);
+            k_gsum<<<ng, 256, 0, s>>>(rt, mm, gsx, gx, gmm, flags, st, p, ntp, ng);
+            k_gout<false><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, gmm, t[0], t[1], st, p, ntp, (uint32_t)n);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
