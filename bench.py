@@ -67,7 +67,7 @@ def parse():
                     help="N>1 only; gloo (+ host-staged exchange) is a test mode for several ranks on one GPU")
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-pointer (PCIe-inclusive) leg")
     ap.add_argument("--host-log2n", type=int, default=30, help="host-pointer leg: keys = 2^host-log2n")
-    ap.add_argument("--host-leg", action="store_true", help=argparse.SUPPRESS)  # the child process of host_path
+    ap.add_argument("--host-leg", default="", help=argparse.SUPPRESS)  # child of host_path: "peer" or "rccl"
     return ap.parse_args()
 
 
@@ -220,35 +220,58 @@ def host_leg_main(args) -> None:
         ok = host_sorted(np, work) and host_fingerprint(np, work) == fp
         return sorted(ts)[len(ts) // 2], ok
 
-    el, ok = timed(lambda a: ls.sort_host(a, algo="auto"), 3)
-    out["single_gpu"] = {"ms": round(el * 1e3, 3), "Mkeys_s": round(n / el / 1e6, 2), "verified": ok,
-                         "call": "labsort_sort_host (order_array)"}
-    if args.gpus > 1:
-        el, ok = timed(lambda a: ls.sort_host_multi(a, args.gpus), 3)
+    if args.host_leg == "peer":
+        el, ok = timed(lambda a: ls.sort_host(a, algo="auto"), 3)
+        out["single_gpu"] = {"ms": round(el * 1e3, 3), "Mkeys_s": round(n / el / 1e6, 2), "verified": ok,
+                             "call": "labsort_sort_host (order_array; pipelined chunks from 2^27 keys)"}
+    if args.gpus > 1 and torch.cuda.device_count() < args.gpus:
+        out[f"error_{args.host_leg}"] = f"{torch.cuda.device_count()} devices visible, {args.gpus} needed"
+    elif args.gpus > 1:
+        devs = list(range(args.gpus))
+        try:
+            el, ok = timed(lambda a: ls.sort_host_ranks(a, devs, transport=args.host_leg), 3)
+        except ls.LabsortError as e:
+            out[f"error_{args.host_leg}"] = str(e)
+            print(json.dumps(out), flush=True)
+            return
         ph, sent = ls.multi_timing()
-        out["multi_gpu"] = {"n_gpus": args.gpus, "ms": round(el * 1e3, 3), "Mkeys_s": round(n / el / 1e6, 2),
-                            "verified": ok, "call": "labsort_sort_host_multi (LABSORT_GPUS=N order_array)",
-                            "phases_ms": {k: round(v, 3) for k, v in ph.items()}, "max_sent_bytes": sent}
+        out[f"multi_gpu_{args.host_leg}"] = {
+            "n_gpus": args.gpus, "ms": round(el * 1e3, 3), "Mkeys_s": round(n / el / 1e6, 2), "verified": ok,
+            "call": "labsort_sort_host_ranks(devices 0..N-1, " + (
+                "RCCL send/recv: what LABSORT_GPUS=N order_array uses)" if args.host_leg == "rccl"
+                else "hipMemcpyPeerAsync exchange)"),
+            "phases_ms": {k: round(v, 3) for k, v in ph.items()}, "max_sent_bytes": sent}
     print(json.dumps(out), flush=True)
 
 
-def host_leg(args, timeout_s: int = 240):
-    """Run the host_path leg in a child process: it opens every GPU it uses itself, and a
-    hang or fault there ends only the child (reported as an error)."""
+def host_leg(args, timeout_s: int = 100):
+    """Run the host_path leg in child processes: each opens the GPUs it uses itself, and a
+    hang or fault there ends only that child (reported as an error).  First the single-GPU
+    sort and the multi-GPU schedule with peer copies, then (N > 1) the same schedule over
+    RCCL, so an RCCL problem cannot cost the other numbers."""
     import subprocess
     drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
             "ROLE_RANK", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")
     env = {k: v for k, v in os.environ.items() if k not in drop}
-    cmd = [sys.executable, os.path.abspath(__file__), "--host-leg", "--gpus", str(args.gpus),
-           "--host-log2n", str(args.host_log2n)]
-    try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
-    except subprocess.TimeoutExpired:
-        return {"error": f"timed out after {timeout_s} s"}
-    for ln in reversed(r.stdout.splitlines()):
-        if ln.startswith("{"):
-            return json.loads(ln)
-    return {"error": f"exit {r.returncode}: {r.stderr.strip()[-400:]}"}
+    out = {}
+    for xfer in ("peer", "rccl") if args.gpus > 1 else ("peer",):
+        cmd = [sys.executable, os.path.abspath(__file__), "--host-leg", xfer, "--gpus", str(args.gpus),
+               "--host-log2n", str(args.host_log2n)]
+        try:
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            out[f"error_{xfer}"] = f"timed out after {timeout_s} s"
+            continue
+        got = None
+        for ln in reversed(r.stdout.splitlines()):
+            if ln.startswith("{"):
+                got = json.loads(ln)
+                break
+        if got is None:
+            out[f"error_{xfer}"] = f"exit {r.returncode}: {r.stderr.strip()[-400:]}"
+        else:
+            out.update(got)
+    return out
 
 
 def main():
