@@ -44,7 +44,9 @@ constexpr int GB = GS_BLOCK, GK = GS_KPT, GT = GS_TILE, GW = GS_BLOCK / WAVE;
 #ifndef LABSORT_GS_WPE
 #define LABSORT_GS_WPE (GS_KPT > 16 ? 2 : 3)
 #endif
-constexpr int GS_WAVES_PER_EU = LABSORT_GS_WPE;  // launch-bounds occupancy hint (workgroups per CU)
+// launch bounds: at least this many waves per SIMD (a VGPR cap).  k_gsweep needs 77
+// VGPRs, k_gcopy 54, so 6 waves per SIMD fit: 3 workgroups of 512 per CU.
+constexpr int GS_WAVES_PER_EU = LABSORT_GS_WPE;
 static_assert(GT == GB * GK && GW * WAVE == GB, "tile shape");
 
 struct GsTables {
