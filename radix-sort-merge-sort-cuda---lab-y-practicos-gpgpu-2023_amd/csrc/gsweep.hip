@@ -345,6 +345,63 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
 }
 
 // ---- scan of the tile rows ------------------------------------------------------------
+// bytewise min / max of packed digit words (byte q = digit q of key ^ flip)
+__device__ __forceinline__ uint32_t bmin4(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = (a >> (8 * q)) & 255u, y = (b >> (8 * q)) & 255u;
+        r |= (x < y ? x : y) << (8 * q);
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t bmax4(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = (a >> (8 * q)) & 255u, y = (b >> (8 * q)) & 255u;
+        r |= (x > y ? x : y) << (8 * q);
+    }
+    return r;
+}
+// Wave-wide bytewise min / max of (mn, mx) pairs, result in every lane.
+__device__ __forceinline__ void wave_minmax4(uint32_t &mn, uint32_t &mx) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        mn = bmin4(mn, __shfl_xor(mn, off));
+        mx = bmax4(mx, __shfl_xor(mx, off));
+    }
+}
+// Digit min / max over `cnt` packed (min, max) pairs into st->dmin / dmax.  Whole
+// block, block-uniform call (barrier).
+template <int BLOCK>
+__device__ __forceinline__ void gs_reduce_minmax(const uint32_t *pairs, uint32_t cnt, uint32_t (*red)[2],
+                                                 GsState *st) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    for (uint32_t i = tid; i < cnt; i += BLOCK) {
+        mn = bmin4(mn, pairs[2 * i]);
+        mx = bmax4(mx, pairs[2 * i + 1]);
+    }
+    wave_minmax4(mn, mx);
+    if (lane == 0) {
+        red[wid][0] = mn;
+        red[wid][1] = mx;
+    }
+    __syncthreads();
+    if (tid < 4u) {
+        uint32_t a = 255u, b = 0u;
+#pragma unroll
+        for (int w = 0; w < BLOCK / WAVE; ++w) {
+            const uint32_t x = (red[w][0] >> (8 * tid)) & 255u, y = (red[w][1] >> (8 * tid)) & 255u;
+            a = x < a ? x : a;
+            b = y > b ? y : b;
+        }
+        st->dmin[tid] = a;
+        st->dmax[tid] = b;
+    }
+}
+
 // k_gsum: column sums of GS_GROUP consecutive tiles' counts, and their exclusive prefix
 // over the groups by decoupled look-back (groups taken in order from a counter, so a
 // group only waits on groups already running; every wait bounded: an expired spin sets
@@ -387,25 +444,29 @@ __global__ __launch_bounds__(256) void k_gsum(const uint32_t *__restrict__ rt, c
     }
     gsx[(size_t)g * 256 + d] = excl;
     if (g + 1 == ngroups) tot[d] = excl + h;
-    if (pass == 0 && d < 4u) {
-        uint32_t mn = 255u, mx = 0u;
-        for (uint32_t t = t0; t < t1; ++t) {
-            const uint32_t a = (mm[2 * t] >> (8 * d)) & 255u, b = (mm[2 * t + 1] >> (8 * d)) & 255u;
-            mn = a < mn ? a : mn;
-            mx = b > mx ? b : mx;
+    if (pass == 0 && d < 64u) {  // the group's tiles' digit min / max, one tile per lane
+        static_assert(GS_GROUP == WAVE, "one tile per lane of wave 0");
+        uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+        if (t0 + d < t1) {
+            mn = mm[2 * (t0 + d)];
+            mx = mm[2 * (t0 + d) + 1];
         }
-        gmm[g * 8 + d] = mn;
-        gmm[g * 8 + 4 + d] = mx;
+        wave_minmax4(mn, mx);
+        if (d == 0) {
+            gmm[2 * g] = mn;
+            gmm[2 * g + 1] = mx;
+        }
     }
 }
 
-// k_gout: the tables of this pass's output buffer, GS_GROUP tiles per workgroup (4
-// threads per digit, 16 tiles each); digit-major writes go through LDS so each is a
-// 256-B line segment.  SMALL (at most GS_SMALL_NG groups): the workgroup sums the
-// earlier groups' and all groups' counts itself from the tile rows, so k_gsum is not
-// launched (the scan is one launch instead of two; at 2^20 keys the launches, not the
-// bytes, set the time).  Workgroup 0 writes the sentinel and, after pass 0, the digit
-// min / max.
+// k_gout: the tables of this pass's output buffer, G tiles per workgroup (4 threads
+// per digit, G/4 tiles each); digit-major writes go through LDS so each is a line
+// segment.  SMALL (at most GS_SMALL_NG scan groups of GS_GROUP tiles): 16-tile
+// workgroups that sum the earlier tiles' and all tiles' counts themselves from the tile
+// rows, so k_gsum is not launched (one scan launch instead of two; at 2^20 keys the
+// launches and latency chains, not the bytes, set the time).  Workgroup 0 writes the
+// sentinel and, after pass 0, the digit min / max.
+constexpr int GS_SGROUP = 16;  // tiles per workgroup of the SMALL scan
 template <bool SMALL>
 __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, const uint32_t *__restrict__ gsx,
                                                const uint32_t *__restrict__ tot, const uint32_t *__restrict__ mm,
@@ -413,14 +474,15 @@ __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, 
                                                GsTables tA, GsTables tB, GsState *st, int pass, uint32_t ntp,
                                                uint32_t n) {
     if (!gs_active(st, pass)) return;
-    __shared__ uint32_t lsb[GS_GROUP][257], srb[GS_GROUP][257];
+    constexpr int G = SMALL ? GS_SGROUP : GS_GROUP, TPQ = G / 4;
+    __shared__ uint32_t lsb[G][257], srb[G][257];
     __shared__ uint32_t part[4][256];
     __shared__ uint32_t pre[2][4][256];
     __shared__ uint32_t wsum[16];
+    __shared__ uint32_t red[16][2];
     const GsTables tb = gs_dst(st, pass) == 1u ? tA : tB;
     const uint32_t g = blockIdx.x, tid = threadIdx.x, d = tid & 255u, q = tid >> 8;
-    constexpr int TPQ = GS_GROUP / 4;
-    const uint32_t t0 = g * GS_GROUP + q * TPQ;
+    const uint32_t t0 = g * G + q * TPQ;
     uint32_t w[TPQ], h = 0;
 #pragma unroll
     for (int i = 0; i < TPQ; ++i) {
@@ -430,13 +492,13 @@ __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, 
     part[q][d] = h;
     uint32_t total = 0, before = 0;
     if constexpr (SMALL) {
-        // counts of digit d in the tiles before this group and in all tiles
+        // counts of digit d in the tiles before this workgroup's and in all tiles
         uint32_t sb = 0, sa = 0;
 #pragma unroll 8
         for (uint32_t t = q; t < ntp; t += 4u) {
             const uint32_t c = rt[(size_t)t * 256 + d] >> 16;
             sa += c;
-            sb += t < g * (uint32_t)GS_GROUP ? c : 0u;
+            sb += t < g * (uint32_t)G ? c : 0u;
         }
         pre[0][q][d] = sb;
         pre[1][q][d] = sa;
@@ -446,32 +508,14 @@ __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, 
             before += pre[0][r][d];
             total += pre[1][r][d];
         }
-        if (g == 0 && tid == 0) tb.ls[(size_t)256 * ntp] = n;  // sentinel start after the last run
-        if (g == 0 && pass == 0 && tid < 4u) {
-            uint32_t mn = 255u, mx = 0u;
-            for (uint32_t t = 0; t < ntp; ++t) {
-                const uint32_t a = (mm[2 * t] >> (8 * tid)) & 255u, b = (mm[2 * t + 1] >> (8 * tid)) & 255u;
-                mn = a < mn ? a : mn;
-                mx = b > mx ? b : mx;
-            }
-            st->dmin[tid] = mn;
-            st->dmax[tid] = mx;
-        }
     } else {
         total = tot[d];
-        before = gsx[(size_t)g * 256 + d];
-        if (g == 0 && tid == 0) tb.ls[(size_t)256 * ntp] = n;  // sentinel start after the last run
-        if (g == 0 && pass == 0 && tid < 4u) {
-            uint32_t mn = 255u, mx = 0u;
-            const uint32_t ng = (ntp + GS_GROUP - 1) / GS_GROUP;
-#pragma unroll 8
-            for (uint32_t gg = 0; gg < ng; ++gg) {
-                mn = gmm[gg * 8 + tid] < mn ? gmm[gg * 8 + tid] : mn;
-                mx = gmm[gg * 8 + 4 + tid] > mx ? gmm[gg * 8 + 4 + tid] : mx;
-            }
-            st->dmin[tid] = mn;
-            st->dmax[tid] = mx;
-        }
+        before = gsx[(size_t)(g * G / GS_GROUP) * 256 + d];
+    }
+    if (g == 0) {
+        if (tid == 0) tb.ls[(size_t)256 * ntp] = n;  // sentinel start after the last run
+        if (pass == 0)  // per tile (SMALL) or per scan group: packed digit min / max pairs
+            gs_reduce_minmax<1024>(SMALL ? mm : gmm, SMALL ? ntp : (ntp + GS_GROUP - 1) / GS_GROUP, red, st);
     }
     // global exclusive digit offsets from the digit totals
     const uint32_t gx = block_excl_scan<1024, 256>(q == 0 ? total : 0u, wsum);
@@ -494,12 +538,14 @@ __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, 
         }
     }
     __syncthreads();
+    // digit-major writes: G consecutive tiles of one digit per lane group
+    constexpr uint32_t LPD = (uint32_t)G, DPW = WAVE / LPD;  // lanes per digit, digits per wave pass
     const uint32_t lane = tid & 63u, wv = tid >> 6;
-    const uint32_t tg = g * GS_GROUP + lane;
+    const uint32_t ti = lane % LPD, tg = g * G + ti;
     if (tg < ntp) {
-        for (uint32_t dd = wv; dd < 256u; dd += 16u) {
-            tb.ls[(size_t)dd * ntp + tg] = lsb[lane][dd];
-            tb.sr[(size_t)dd * ntp + tg] = srb[lane][dd];
+        for (uint32_t dd = wv * DPW + lane / LPD; dd < 256u; dd += 16u * DPW) {
+            tb.ls[(size_t)dd * ntp + tg] = lsb[ti][dd];
+            tb.sr[(size_t)dd * ntp + tg] = srb[ti][dd];
         }
     }
 }
@@ -548,7 +594,7 @@ GsLayout gs_layout(size_t n) {
     L.off_gx = o;
     o = al(o + 257 * 4);
     L.off_gmm = o;
-    o = al(o + ng * 8 * 4);
+    o = al(o + ng * 2 * 4);
     for (int s = 0; s < 2; ++s) {
         L.off_ls[s] = o;
         o = al(o + (ne + 1) * 4);
@@ -584,7 +630,8 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
         if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (ng <= (uint32_t)GS_SMALL_NG) {
-            k_gout<true><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, gmm, t[0], t[1], st, p, ntp, (uint32_t)n);
+            k_gout<true><<<(ntp + GS_SGROUP - 1) / GS_SGROUP, 1024, 0, s>>>(rt, gsx, gx, mm, gmm, t[0], t[1], st, p,
+                                                                           ntp, (uint32_t)n);
         } else {
             k_gsum<<<ng, 256, 0, s>>>(rt, mm, gsx, gx, gmm, flags, st, p, ntp, ng);
             k_gout<false><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, gmm, t[0], t[1], st, p, ntp, (uint32_t)n);
