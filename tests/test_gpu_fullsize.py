@@ -86,3 +86,41 @@ def test_fullsize_inplace_repeat(ls, torch_gpu):
         ls.sort_device(t, o, n, algo="radix", workspace=ws)
         torch.cuda.synchronize()
         assert sha(o.cpu().numpy().view(np.uint32)) == c["sha256_sorted_u32"]
+
+
+@pytest.mark.parametrize("name,impl", [("config3_2^28_u32", "gather"), ("2^24_mod1000", "gather"),
+                                       ("config2_2^20_u32", "onesweep"), ("2^24_mod1000", "onesweep")])
+def test_fullsize_sha_radix_impls(ls, torch_gpu, monkeypatch, name, impl):
+    """Both radix implementations at full size, outside the window where AUTO/RADIX
+    picks them (gathered passes at 2^28, onesweep at 2^20 and 2^24)."""
+    torch = torch_gpu
+    monkeypatch.setenv("LABSORT_RADIX_IMPL", impl)
+    c = BIG[name]
+    n = 1 << c["log2n"]
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, c["seed"], c["dist"])
+    ws = torch.empty(ls.workspace_bytes(n, "radix"), dtype=torch.uint8, device="cuda")
+    o = torch.empty_like(t)
+    ls.sort_device(t, o, n, key="u32", algo="radix", workspace=ws)
+    torch.cuda.synchronize()
+    ls.workspace_status(ws, n, "radix")
+    assert sha(o.cpu().numpy().view(np.uint32)) == c["sha256_sorted_u32"]
+
+
+@pytest.mark.parametrize("name", ["config3_2^28_u32", "config5_2^30_u32"])
+def test_fullsize_host_pipeline(ls, torch_gpu, name):
+    """order_array's host-pointer path at full size: from 2^27 keys the pipelined
+    chunks (radix chunk sorts, half merges, final merge by ranges under D2H); at 2^30
+    AUTO sorts the 2^27-key chunks by radix although the whole array is past the radix
+    limit."""
+    torch = torch_gpu
+    c = BIG[name]
+    n = 1 << c["log2n"]
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, c["seed"], c["dist"])
+    a = t.cpu().numpy().view(np.uint32)
+    del t
+    torch.cuda.empty_cache()
+    ls.sort_host(a, algo="auto")
+    assert int(a[0]) == c["first"] and int(a[-1]) == c["last"] and int(a[n // 2]) == c["median"]
+    assert sha(a) == c["sha256_sorted_u32"]
