@@ -52,7 +52,8 @@ if len(sys.argv) > 1 and sys.argv[1] == "time":
     print(f"{os.path.basename(os.environ.get('LABSORT_LIBRARY', 'default'))}: gather {tg:.3f} ms  onesweep {to:.3f} ms")
     sys.exit(0)
 if len(sys.argv) > 1 and sys.argv[1] == "prof":
-    run(1 << int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 28, "u32", "u32", "gather", reps=10)
+    run(1 << int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 28, sys.argv[3] if len(sys.argv) > 3 else "u32", "u32",
+        sys.argv[4] if len(sys.argv) > 4 else "gather", reps=10)
     sys.exit(0)
 for n, dist, key in [(1 << 22, "u32", "u32"), ((1 << 22) + 12345, "mod100", "i32"), ((1 << 24) + 7, "u32", "i32"),
                      (1 << 24, "const", "u32"), (1 << 24, "lowbits", "u32"), (1 << 28, "u32", "u32")]:

@@ -94,10 +94,10 @@ class HipOps(Ops):
 
     def __init__(self, ls, key: str = "u32", local_algo: str = "radix", stream=None, kway: bool = True):
         self.ls, self.key, self.algo, self.stream = ls, key, local_algo, stream
-        # kway: merge the received runs in one K-way pass (labsort_merge_runs) instead of
-        # a tree of labsort_merge calls.  Measured on MI355X for 2^28 keys in p runs
-        # (profiles/r15_dist_merge_step.jsonl): p = 2 / 4 / 8: K-way 0.62 / 1.24 /
-        # 1.91 ms, tree 0.75 / 1.47 / 2.28 ms
+        # kway: merge the received runs with labsort_merge_runs (pair passes over explicit
+        # runs in C++) instead of a Python tree of labsort_merge calls.  Measured on
+        # MI355X for 2^28 keys in p runs (profiles/r17_dist_merge_step.jsonl): p = 2 / 4 /
+        # 8: 0.53 / 1.04 / 1.66 ms, tree 0.75 / 1.45 / 2.22 ms
         self.kway = kway
         self._ws = None
         self._part = None
