@@ -74,6 +74,26 @@ __device__ __forceinline__ bool lds_lane_ordered(uint32_t *scratch, uint32_t lan
     return __ballot(!ok) == 0ull;
 }
 
+// Stable rank of digit d among this wave's keys so far, by one returning LDS atomic
+// add on the wave's counter wh[d] (lane-ordered: see lds_lane_ordered).  A digit the
+// whole wave shares (sorted or nearly sorted input: the high digits of 64 consecutive
+// keys) takes one add of 64 instead of 64 adds serialised on one address.  All 64
+// lanes active.
+#ifndef LABSORT_RANK_UNIFORM
+#define LABSORT_RANK_UNIFORM 1
+#endif
+__device__ __forceinline__ uint32_t wave_atomic_rank(uint32_t *wh, uint32_t d, uint32_t lane) {
+    if (LABSORT_RANK_UNIFORM) {
+        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+        if (__ballot(d != d0) == 0ull) {
+            uint32_t b = 0;
+            if (lane == 0) b = __hip_atomic_fetch_add(wh + d0, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            return __builtin_amdgcn_readfirstlane(b) + lane;
+        }
+    }
+    return __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 // Exclusive scan over the first R threads of the block (value v in thread tid < R,
 // others pass 0).  Must be called by every thread (contains a barrier when R > 64).
 template <int BLOCK, int R>

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
         const uint32_t d = ((k[j] ^ flip) >> shift) & 255u;
         uint32_t r;
         if (atomic_rank) {
-            r = __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+            r = wave_atomic_rank(wh, d, lane);
         } else {
             const uint64_t m = match8(d);
             const uint32_t pre = mbcnt64(m);

@@ -199,15 +199,15 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
 #pragma unroll
         for (int p = 0; p < 3; ++p) atomicAdd(&hj[p * JF + ((k >> (8 * p + 4)) & (JF - 1))], 1u);
     };
-    // 16 keys of one lane: digit 0 as above (replicated slots: contention-free for any
-    // data).  A joint field that is the same for all 16 keys (the high fields of small
-    // keys: %100, %1000 inputs) is added once, 16 at a time: with one add per key, 64
-    // lanes on one counter serialise, and the kernel took 1.85-1.99 ms instead of
-    // 0.27 ms at 2^28 (r19).  The test compares the first and last keys' fields and
-    // only then the rest, so uniform keys pay one compare per 16 keys and field.
-#ifndef LABSORT_HS_RLE
-#define LABSORT_HS_RLE 7  // joint fields with the 16-key constant test (bit p)
-#endif
+    // 16 keys of one lane (4 uint4 of 4 consecutive keys): digit 0 as above
+    // (replicated slots: contention-free for any data).  Joint fields: with one add per
+    // key, keys whose field repeats (small keys: %100, %1000; sorted or clustered input)
+    // put many lanes on one LDS counter, which serialises them -- at 2^28 the kernel
+    // took 1.85-1.99 ms (%1000, %100) and 1.06 ms (sorted) instead of 0.27 ms (r19).
+    // So a field that is the same for a lane's 16 keys, or for one uint4, is added once.
+    // The tests run only in waves where some lane's top field repeats within its first
+    // uint4 (one compare and a ballot per 16 keys): uniform keys keep the plain adds.
+    auto fld = [&](uint32_t k, int p) { return (k >> (8 * p + 4)) & (JF - 1); };
     auto count16 = [&](const uint4 (&c)[4]) {
         uint32_t k[16];
 #pragma unroll
@@ -219,19 +219,35 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) atomicAdd(&h[(k[j] & 255u) * SL + slot], 1u);
+        if (__ballot(fld(k[0], 2) == fld(k[3], 2)) == 0ull) {  // no repeats here
+#pragma unroll
+            for (int p = 0; p < 3; ++p)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) atomicAdd(&hj[p * JF + fld(k[j], p)], 1u);
+            return;
+        }
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
-            const uint32_t f0 = (k[0] >> (8 * p + 4)) & (JF - 1);
-            bool same = ((LABSORT_HS_RLE >> p) & 1) && ((k[15] >> (8 * p + 4)) & (JF - 1)) == f0;
-            if (same) {  // first and last agree: check the rest (rarely taken on uniform keys)
+            const uint32_t f0 = fld(k[0], p);
+            bool same = fld(k[15], p) == f0;
+            if (same) {  // first and last agree: check the rest
 #pragma unroll
-                for (int j = 1; j < 15; ++j) same &= ((k[j] >> (8 * p + 4)) & (JF - 1)) == f0;
+                for (int j = 1; j < 15; ++j) same &= fld(k[j], p) == f0;
             }
             if (same) {
                 atomicAdd(&hj[p * JF + f0], 16u);
-            } else {
+                continue;
+            }
 #pragma unroll
-                for (int j = 0; j < 16; ++j) atomicAdd(&hj[p * JF + ((k[j] >> (8 * p + 4)) & (JF - 1))], 1u);
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t fa = fld(k[4 * u], p);
+                const bool s4 = fld(k[4 * u + 3], p) == fa && fld(k[4 * u + 1], p) == fa && fld(k[4 * u + 2], p) == fa;
+                if (s4) {
+                    atomicAdd(&hj[p * JF + fa], 4u);
+                } else {
+#pragma unroll
+                    for (int j = 4 * u; j < 4 * u + 4; ++j) atomicAdd(&hj[p * JF + fld(k[j], p)], 1u);
+                }
             }
         }
     };
@@ -666,10 +682,19 @@ __device__ __forceinline__ uint32_t osp_load(const uint32_t *p) {
     else return *p;
 }
 
+// LDS index of tile slot i in the reorder buffer: one pad word per 32 slots, so a
+// wave's stores to slots 64 apart (one per digit: sorted or strided input, where every
+// digit of a tile has the same count) spread over the banks instead of all landing on
+// one, and the slot-order read-back stays conflict-free.
+#ifndef LABSORT_OSP_PAD
+#define LABSORT_OSP_PAD 1
+#endif
+__device__ __forceinline__ uint32_t osp_pad(uint32_t i) { return LABSORT_OSP_PAD ? i + (i >> 5) : i; }
+
 template <bool MATCH>
 struct OspSmem {
     static constexpr int R = 256, W = OSP_BLOCK / WAVE, TILE = OSP_TILE;
-    uint32_t keys[TILE];
+    uint32_t keys[TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0)];  // padded: see osp_pad
     uint32_t wh[W * R];
     uint64_t match[MATCH ? W * R : 1];
     uint32_t probe[WAVE];
@@ -848,7 +873,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
                 if (atomic_rank) {
-                    const uint32_t r = __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                    const uint32_t r = wave_atomic_rank(wh, d, lane);
                     rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
                 } else {
                     const uint64_t m = RANK != OSP_RANK_BALLOT ? lds_peers(wm + d, lane) : match8(d);
@@ -976,11 +1001,11 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         OSP_T(7, 0);
 #pragma unroll
         for (int j = 0; j < KPT; ++j)
-            sm.keys[wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = kB[j];
+            sm.keys[osp_pad(wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu))] = kB[j];
         __syncthreads();  // (4) B reordered in LDS
         OSP_T(8, 0);  // reorder
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[j * OSP_BLOCK + tid];
+        for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * OSP_BLOCK + tid)];
         // each wave clears its own counters (no barrier before the next ranking)
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
         OSP_T(9, 2);  // readback
@@ -1107,7 +1132,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
             const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
             uint32_t r;
             if (atomic_rank) {
-                r = __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+                r = wave_atomic_rank(wh, d, lane);
             } else {
                 const uint64_t m = match8(d);
                 const uint32_t pre = mbcnt64(m);
