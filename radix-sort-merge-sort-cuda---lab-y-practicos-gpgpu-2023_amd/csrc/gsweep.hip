@@ -175,9 +175,14 @@ __device__ __forceinline__ void gs_gather(const uint32_t *__restrict__ src, cons
     }
 }
 
+// LDS word of tile slot i in the reorder buffer: 4 pad words per 32 slots (16-B
+// aligned, for the uint4 write-out).  In a sorted tile every digit holds 32 keys, so a
+// wave's reorder stores land 32 slots apart: one bank unpadded, 8 banks padded.
+__device__ __forceinline__ uint32_t gs_pad(uint32_t i) { return i + ((i >> 5) << 2); }
+
 struct GsSmem {
     union {  // the run tables are only read while the tile is gathered, before the reorder
-        uint32_t keys[GT];
+        uint32_t keys[GT + GT / 8];
         GsRuns g;
     };
     uint32_t wh[GW * 256];
@@ -327,19 +332,22 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
 #pragma unroll
     for (int j = 0; j < GK; ++j) {
         const uint32_t d = ((k[j] ^ flip) >> shift) & 255u;
-        sm.keys[wh[d] + ((rk[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = k[j];
+        sm.keys[gs_pad(wh[d] + ((rk[j / 2] >> ((j & 1) * 16)) & 0xFFFFu))] = k[j];
     }
     __syncthreads();  // (3) tile sorted in LDS
     if (nvalid == (uint32_t)GT) {
         const uint4 *s4 = reinterpret_cast<const uint4 *>(sm.keys);
         uint4 *d4 = reinterpret_cast<uint4 *>(dst + L0);
 #pragma unroll
-        for (int j = 0; j < GK / 4; ++j) d4[j * GB + tid] = s4[j * GB + tid];
+        for (int j = 0; j < GK / 4; ++j) {
+            const uint32_t q = (uint32_t)j * GB + tid;  // uint4 q = slots 4q..4q+3, one 32-slot row
+            d4[q] = s4[q + (q >> 3)];
+        }
     } else {
 #pragma unroll
         for (int j = 0; j < GK; ++j) {
             const uint32_t i = (uint32_t)j * GB + tid;
-            if (i < nvalid) dst[L0 + i] = sm.keys[i];
+            if (i < nvalid) dst[L0 + i] = sm.keys[gs_pad(i)];
         }
     }
 }
