@@ -6,7 +6,7 @@ import torch
 ls = importlib.import_module("radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd")
 for lg in [int(x) for x in os.environ.get("LOG2NS", "16 18 20 22 24 26 28").split()]:
     n = 1 << lg
-    k = torch.empty(n, dtype=torch.int32, device="cuda"); ls.fill(k, n, 0x5EED0011, "u32")
+    k = torch.empty(n, dtype=torch.int32, device="cuda"); ls.fill(k, n, 0x5EED0011, os.environ.get("DIST", "u32"), param=int(os.environ.get("PARAM", "0")))
     v = torch.arange(n, dtype=torch.int32, device="cuda")
     ko, vo = torch.empty_like(k), torch.empty_like(v)
     row = [f"2^{lg}"]

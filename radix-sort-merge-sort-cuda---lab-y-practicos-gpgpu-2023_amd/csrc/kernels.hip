@@ -487,11 +487,20 @@ __global__ __launch_bounds__(256) void k_final_copy(Bufs b, const Plan *__restri
 // ---------------------------------------------------------------------------------
 // one LSD radix pass ("onesweep"): rank, look-back, LDS reorder, coalesced scatter
 // ---------------------------------------------------------------------------------
+// LDS index of tile slot i in the reorder buffer: one pad word per 32 slots, so a
+// wave's stores to slots 64 apart (one per digit: sorted or strided input, where every
+// digit of a tile has the same count) spread over the banks instead of all landing on
+// one, and the slot-order read-back stays conflict-free.
+#ifndef LABSORT_OSP_PAD
+#define LABSORT_OSP_PAD 1
+#endif
+__device__ __forceinline__ uint32_t osp_pad(uint32_t i) { return LABSORT_OSP_PAD ? i + (i >> 5) : i; }
+
 template <int BITS, int BLOCK, int KPT, bool KV = false>
 struct OsSmem {
     static constexpr int R = 1 << BITS, W = BLOCK / WAVE, TILE = BLOCK * KPT;
-    uint32_t keys[TILE];
-    uint32_t vals[KV ? TILE : 1];  // key/value: payloads reordered with their keys
+    uint32_t keys[TILE + TILE / 32];  // padded (osp_pad)
+    uint32_t vals[KV ? TILE + TILE / 32 : 1];  // key/value: payloads reordered with their keys
     uint32_t whist[W * R];
     uint32_t gscan[R];
     uint32_t dstart[R];
@@ -584,7 +593,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
     // reorder the tile by digit in LDS
 #pragma unroll
     for (int j = 0; j < KPT; ++j) {
-        const uint32_t pos = sm.dstart[dig[j]] + wh[dig[j]] + rank[j];
+        const uint32_t pos = osp_pad(sm.dstart[dig[j]] + wh[dig[j]] + rank[j]);
         sm.keys[pos] = k[j];
         if constexpr (KV) sm.vals[pos] = v[j];
     }
@@ -619,10 +628,10 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
     for (int j = 0; j < KPT; ++j) {
         const uint32_t i = (uint32_t)j * BLOCK + tid;
         if (i < nvalid) {
-            const uint32_t key = sm.keys[i];
+            const uint32_t key = sm.keys[osp_pad(i)];
             const uint32_t d = ((key ^ flip) >> shift) & RM;
             out[sm.delta[d] + i] = key;
-            if constexpr (KV) vbufs.p[plan->dst[pass]][sm.delta[d] + i] = sm.vals[i];
+            if constexpr (KV) vbufs.p[plan->dst[pass]][sm.delta[d] + i] = sm.vals[osp_pad(i)];
         }
     }
 }
@@ -682,14 +691,7 @@ __device__ __forceinline__ uint32_t osp_load(const uint32_t *p) {
     else return *p;
 }
 
-// LDS index of tile slot i in the reorder buffer: one pad word per 32 slots, so a
-// wave's stores to slots 64 apart (one per digit: sorted or strided input, where every
-// digit of a tile has the same count) spread over the banks instead of all landing on
-// one, and the slot-order read-back stays conflict-free.
-#ifndef LABSORT_OSP_PAD
-#define LABSORT_OSP_PAD 1
-#endif
-__device__ __forceinline__ uint32_t osp_pad(uint32_t i) { return LABSORT_OSP_PAD ? i + (i >> 5) : i; }
+
 
 template <bool MATCH>
 struct OspSmem {
