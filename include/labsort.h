@@ -94,6 +94,10 @@ size_t labsort_workspace_bytes(size_t n, int algo);
 int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, int algo, void *d_workspace,
                         size_t workspace_bytes, void *stream);
 /* Host pointer in/out, synchronous: the order_array contract (lab.cu:303).
+ * From 2^27 keys the copies are pipelined: 8 chunks copied H2D while earlier chunks
+ * sort (each by `algo` resolved at the chunk's size), two half merges, and the final
+ * merge by 8 diagonal ranges whose D2H copies start as each range lands
+ * (LABSORT_HOST_PIPE=0 turns it off, =1 forces it from 2^16 keys).
  * Returns LABSORT_ERR_DEVICE when a kernel reported an internal error. */
 int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo);
 /* Device-side status of the last labsort_sort_device(n, algo) that used d_workspace:
