@@ -31,10 +31,17 @@ constexpr int HIST_BLOCK = 1024;
 #define LABSORT_OSP_LBW2 4
 #endif
 #ifndef LABSORT_OSP_PREFETCH
-#define LABSORT_OSP_PREFETCH 0
+#define LABSORT_OSP_PREFETCH 1  // r19 with nontemporal loads: 2^28 sort 2.45 -> 2.33 ms (without them it was slower)
 #endif
 #ifndef LABSORT_OSP_NT
-#define LABSORT_OSP_NT 0
+#define LABSORT_OSP_NT 0  // bit 0: nontemporal scatter stores (measured slower, r19)
+#endif
+// Nontemporal key loads per kernel family (ld_stream in devutil.h).  r19 A/B at 2^28:
+// onesweep passes 0.556 -> 0.523 ms, the upfront histogram ~0.02 ms faster; the tile
+// sort, merge pass and gathered passes were slightly slower with them (not set).
+constexpr int NT_OSP = 1, NT_HIST = 2, NT_TILE = 4, NT_MERGE = 8, NT_GS = 16, NT_OS = 32;
+#ifndef LABSORT_NT_LOADS
+#define LABSORT_NT_LOADS 3  // NT_OSP | NT_HIST
 #endif
 #ifndef LABSORT_OSP_XCD
 #define LABSORT_OSP_XCD 1
@@ -48,6 +55,13 @@ constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 16384 keys per tile
 constexpr int OSP_LBW = LABSORT_OSP_LBW;    // look-back window of the first round (predecessor tiles)
 constexpr int OSP_LBW2 = LABSORT_OSP_LBW2;  // look-back window of the later rounds
 constexpr bool OSP_PREFETCH = LABSORT_OSP_PREFETCH != 0;  // next tile's keys loaded one iteration ahead
+// A's keys are scattered straight from the LDS reorder buffer (read at scatter
+// time, before B's reorder overwrites it) instead of being read back into registers at the
+// end of the previous iteration: 16 VGPRs fewer across the look-back
+#ifndef LABSORT_OSP_LDS_SCATTER
+#define LABSORT_OSP_LDS_SCATTER 0  // r19: slower (2.33 -> 2.59 ms with prefetch, 2.46 without)
+#endif
+constexpr bool OSP_LDS_SCATTER = LABSORT_OSP_LDS_SCATTER != 0;
 constexpr int OSP_RANK_BALLOT = 0, OSP_RANK_MATCH = 1, OSP_RANK_ATOMIC = 2;  // k_onesweep_p<RANK, HIST_FIRST>
 constexpr int OSP_SEG_LATER = 1;  // 1: digit-group segments after the first active pass (LABSORT_SEG)
 constexpr int OSP_DEFAULT_VARIANT = 4;          // variant = RANK * 2 + HIST_FIRST

@@ -18,6 +18,27 @@ __device__ __forceinline__ void st_agent(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Streamed key loads (LABSORT_NT_LOADS, one bit per kernel family, NT_*): a pass reads
+// each key once, so its loads are issued nontemporal and the L2 keeps its capacity for
+// the lines being written.  For the onesweep scatter that matters: the partial 64-B
+// granules two consecutive tiles write at a digit-run boundary meet in the L2 before
+// write-back instead of reaching HBM as read-modify-writes.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+template <int BIT>
+__device__ __forceinline__ uint32_t ld_stream(const uint32_t *p) {
+    if constexpr ((LABSORT_NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int BIT>
+__device__ __forceinline__ uint4 ld_stream4(const uint4 *p) {
+    if constexpr ((LABSORT_NT_LOADS & BIT) != 0) {
+        const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+        return make_uint4(v.x, v.y, v.z, v.w);
+    } else {
+        return *p;
+    }
+}
+
 // Lanes whose digit equals mine (all 64 lanes active): BITS ballots.
 template <int BITS>
 __device__ __forceinline__ uint64_t match_digit(uint32_t d) {

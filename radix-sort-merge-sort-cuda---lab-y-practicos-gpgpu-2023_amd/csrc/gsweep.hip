@@ -149,10 +149,10 @@ __device__ __forceinline__ void gs_gather(const uint32_t *__restrict__ src, cons
         }
         if (nvalid == (uint32_t)GT) {
 #pragma unroll
-            for (int j = 0; j < GK; ++j) k[j] = src[addr[j]];
+            for (int j = 0; j < GK; ++j) k[j] = ld_stream<NT_GS>(src + addr[j]);
         } else {
 #pragma unroll
-            for (int j = 0; j < GK; ++j) k[j] = pw + (uint32_t)j * WAVE < nvalid ? src[addr[j]] : sentinel;
+            for (int j = 0; j < GK; ++j) k[j] = pw + (uint32_t)j * WAVE < nvalid ? ld_stream<NT_GS>(src + addr[j]) : sentinel;
         }
     } else {
         // many (mostly empty) runs: each lane searches the tables directly
@@ -167,7 +167,7 @@ __device__ __forceinline__ void gs_gather(const uint32_t *__restrict__ src, cons
                     if (tb.ls[mid] <= P) lo = mid;
                     else hi = mid;
                 }
-                k[j] = src[tb.sr[lo] + (P - tb.ls[lo])];
+                k[j] = ld_stream<NT_GS>(src + tb.sr[lo] + (P - tb.ls[lo]));
             } else {
                 k[j] = sentinel;
             }

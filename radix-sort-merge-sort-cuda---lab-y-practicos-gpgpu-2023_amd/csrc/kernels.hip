@@ -269,19 +269,19 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
         uint4 c[4], x[4];
         if (i + 3 * HIST_BLOCK < nv) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) c[u] = v[i + u * HIST_BLOCK];
+            for (int u = 0; u < 4; ++u) c[u] = ld_stream4<NT_HIST>(v + i + u * HIST_BLOCK);
         }
         for (; i + 3 * HIST_BLOCK < nv; i += 4 * HIST_BLOCK) {
             if (i + 7 * HIST_BLOCK < nv) {
 #pragma unroll
-                for (int u = 0; u < 4; ++u) x[u] = v[i + (4 + u) * HIST_BLOCK];
+                for (int u = 0; u < 4; ++u) x[u] = ld_stream4<NT_HIST>(v + i + (4 + u) * HIST_BLOCK);
             }
             count16(c);
 #pragma unroll
             for (int u = 0; u < 4; ++u) c[u] = x[u];
         }
         for (; i < nv; i += HIST_BLOCK) {
-            const uint4 x = v[i];
+            const uint4 x = ld_stream4<NT_HIST>(v + i);
             count(x.x); count(x.y); count(x.z); count(x.w);
         }
         for (size_t r = vbeg + nv * 4 + threadIdx.x; r < end; r += HIST_BLOCK) count(keys[r]);
@@ -549,12 +549,12 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
     const uint32_t wbase = base + wid * (KPT * WAVE) + lane;
     if (nvalid == (uint32_t)TILE) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = in[wbase + j * WAVE];
+        for (int j = 0; j < KPT; ++j) k[j] = ld_stream<NT_OS>(in + wbase + j * WAVE);
     } else {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t idx = wbase + j * WAVE;
-            k[j] = idx < n ? in[idx] : sentinel;
+            k[j] = idx < n ? ld_stream<NT_OS>(in + idx) : sentinel;
         }
     }
     uint32_t v[KV ? KPT : 1];
@@ -681,15 +681,12 @@ __device__ unsigned long long g_osp_stamps[16];
 #endif
 
 // key stream accesses of the onesweep pass (LABSORT_OSP_NT bit 0: nontemporal scatter
-// stores, bit 1: nontemporal key loads)
+// stores; key loads: LABSORT_NT_LOADS & NT_OSP)
 __device__ __forceinline__ void osp_store(uint32_t *p, uint32_t v) {
     if constexpr (LABSORT_OSP_NT & 1) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
-__device__ __forceinline__ uint32_t osp_load(const uint32_t *p) {
-    if constexpr (LABSORT_OSP_NT & 2) return __builtin_nontemporal_load(p);
-    else return *p;
-}
+__device__ __forceinline__ uint32_t osp_load(const uint32_t *p) { return ld_stream<NT_OSP>(p); }
 
 
 
@@ -967,13 +964,15 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
-                    osp_store(out + sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i, kA[j]);
+                    const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
+                    osp_store(out + sm.delta[((key ^ flip) >> shift) & 255u] + i, key);
                 }
             } else {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
-                    if (i < nvalidA) osp_store(out + sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i, kA[j]);
+                    const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
+                    if (i < nvalidA) osp_store(out + sm.delta[((key ^ flip) >> shift) & 255u] + i, key);
                 }
             }
         }
@@ -1006,8 +1005,10 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             sm.keys[osp_pad(wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu))] = kB[j];
         __syncthreads();  // (4) B reordered in LDS
         OSP_T(8, 0);  // reorder
+        if (!OSP_LDS_SCATTER) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * OSP_BLOCK + tid)];
+            for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * OSP_BLOCK + tid)];
+        }
         // each wave clears its own counters (no barrier before the next ranking)
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
         OSP_T(9, 2);  // readback
@@ -1079,7 +1080,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
     }
     if (full) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = in[wbase + j * WAVE];
+        for (int j = 0; j < KPT; ++j) k[j] = ld_stream<NT_TILE>(in + wbase + j * WAVE);
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             a &= k[j] ^ flip;
@@ -1090,7 +1091,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
         for (int j = 0; j < KPT; ++j) {
             const uint32_t idx = wbase + j * WAVE;
             const bool ok = idx < n;
-            k[j] = ok ? in[idx] : sentinel;
+            k[j] = ok ? ld_stream<NT_TILE>(in + idx) : sentinel;
             const uint32_t x = k[j] ^ flip;
             a &= ok ? x : ~0u;
             o |= ok ? x : 0u;
@@ -1385,7 +1386,7 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         for (int j = 0; j < KPT; ++j) {
             const uint32_t k = tid + (uint32_t)j * BLOCK;
             const uint32_t a = k < q.la ? q.sa + k : q.sb + (k - q.la);
-            v[j] = k < q.tot ? src[a] : 0u;
+            v[j] = k < q.tot ? ld_stream<NT_MERGE>(src + a) : 0u;
             if constexpr (KV) vv[j] = k < q.tot ? vsrc[a] : 0u;
         }
     };
