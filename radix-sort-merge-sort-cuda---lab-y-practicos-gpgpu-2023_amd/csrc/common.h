@@ -25,10 +25,10 @@ constexpr int HIST_BLOCK = 1024;
 #define LABSORT_OSP_KPT 16
 #endif
 #ifndef LABSORT_OSP_LBW
-#define LABSORT_OSP_LBW 4
+#define LABSORT_OSP_LBW 8  // r20 sweep (2^28, with prefetch): 2 0.562, 4 0.505, 6 0.487, 8 0.486, 10 0.530, 16 0.709 ms per pass
 #endif
 #ifndef LABSORT_OSP_LBW2
-#define LABSORT_OSP_LBW2 4
+#define LABSORT_OSP_LBW2 8
 #endif
 #ifndef LABSORT_OSP_PREFETCH
 #define LABSORT_OSP_PREFETCH 1  // r19 with nontemporal loads: 2^28 sort 2.45 -> 2.33 ms (without them it was slower)
