@@ -79,7 +79,10 @@ static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass til
 // decoupled look-back chain; a segment's base offsets come from histograms the
 // upfront histogram kernel computes (see k_hist_seg / k_plan8).
 constexpr int NSEG = 16;
-constexpr int HS_BPS = 32;  // histogram workgroups per position segment (2 per CU: 80 KB LDS each)
+#ifndef LABSORT_HS_BPS
+#define LABSORT_HS_BPS 16  // r21: k_hist_seg at 2^28 0.273 ms (32), 0.255 (16), 0.420 (8)
+#endif
+constexpr int HS_BPS = LABSORT_HS_BPS;  // histogram workgroups per position segment (80 KB LDS each)
 constexpr size_t HS_MIN_KEYS = 65536;  // fewest keys per histogram workgroup below 2^25 keys
 #ifndef LABSORT_HS_ROT
 #define LABSORT_HS_ROT 1
