@@ -198,7 +198,10 @@ constexpr int GS_KPT = LABSORT_GS_KPT;
 constexpr int GS_TILE = GS_BLOCK * GS_KPT;      // 8192 keys
 constexpr int GS_KMAX = 1024;                   // runs per tile listed in LDS (else per-lane search)
 constexpr int GS_GROUP = 64;                    // tiles per scan workgroup
-constexpr int GS_SMALL_NG = 2;                  // up to this many groups (2^20 keys): one scan launch per pass
+#ifndef LABSORT_GS_SMALL_NG
+#define LABSORT_GS_SMALL_NG 2
+#endif
+constexpr int GS_SMALL_NG = LABSORT_GS_SMALL_NG;  // up to this many groups (2^20 keys): one scan launch per pass
 constexpr size_t GS_MIN_N = (size_t)1 << 16;    // LABSORT_ALGO_RADIX uses it for GS_MIN_N <= n < GS_MAX_N
 constexpr size_t GS_MAX_N = (size_t)1 << 26;    // (onesweep outside; measured crossovers)
 struct GsLayout {
