@@ -234,6 +234,13 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
 #pragma unroll
                 for (int j = 1; j < 15; ++j) same &= fld(k[j], p) == f0;
             }
+            // the whole wave on one field (sorted or clustered input): one add for it
+            const uint32_t w0 = __builtin_amdgcn_readfirstlane(f0);
+            const uint64_t act = __ballot(true);
+            if (__ballot(same && f0 == w0) == act) {
+                if (mbcnt64(act) == 0u) atomicAdd(&hj[p * JF + w0], 16u * (uint32_t)__popcll(act));
+                continue;
+            }
             if (same) {
                 atomicAdd(&hj[p * JF + f0], 16u);
                 continue;
