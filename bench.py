@@ -10,10 +10,13 @@ generator, seed 0x5EED0003) and stay resident in HBM; the sort is out of place
 so every step sorts the same input.
 
 N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): the
-merge-sort path of the north_star.  Each rank holds a fixed 2^log2n-key shard
-(weak scaling), sorts it locally with the radix kernels, then the splitter
-exchange (or, --exchange pairwise, the bitonic merge-split network) moves keys
-over RCCL send/recv (dist.py).  value = all ranks' keys / max-over-ranks time.
+merge-sort path of the north_star through the product's C-ABI: every rank calls
+labsort_dist_sort on its communicator (labsort_comm_init_rccl, rank 0's unique id
+broadcast over torch.distributed).  Each rank holds a fixed 2^log2n-key shard (weak
+scaling), sorts it locally with the radix kernels, then the splitter exchange moves
+keys by grouped ncclSend/ncclRecv and each rank merges its received runs
+(csrc/dist_plan.h).  --exchange pairwise runs the Python bitonic merge-split network
+(dist.py) instead.  value = all ranks' keys / max-over-ranks time.
 
 host_path (after the timed region, rank 0, in a child process): the reference's
 own calling convention -- a pageable host int* of 2^30 keys (BASELINE config 5)
@@ -171,6 +174,91 @@ def cpu_baseline(budget_s: float, n: int, ls):
                                       f"{treps} x 2^24 keys, {tt:.1f} s"}}
 
 
+def _config1_fixture():
+    return json.load(open(os.path.join(REPO, "tests", "golden", "big.json")))["config1_2^16_u32"]
+
+
+def _sha(np, x) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(x).tobytes()).hexdigest()
+
+
+def _median_s(fn, reps: int) -> float:
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2]
+
+
+def config1_cpu(ls):
+    """BASELINE config 1 on the CPU reference path (part of cpu_baseline): n=2^16 uniform
+    uint32 keys (main.cpp's largest size) sorted by std::sort (the oracle, one core) and
+    by order_with_trust (rocThrust's host sort, lab.cu:404-406; CPU, F7), each checked
+    against the committed fixture (tests/golden/big.json)."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle as O  # test infrastructure: the CPU baseline leg only
+    c = _config1_fixture()
+    n = 1 << c["log2n"]
+    a = O.gen(n, c["seed"], c["dist"])
+    ok = _sha(np, a) == c["sha256_input"] and _sha(np, O.sort_u32(a)) == c["sha256_sorted_u32"]
+    t_std = O.time_sort_u32(a, threads=1, reps=200) / 200
+    b = a.view(np.int32).copy()
+
+    def trust():
+        np.copyto(b, a.view(np.int32))
+        ls.order_with_trust(b)
+    t_trust = _median_s(trust, 50)
+    ok = ok and _sha(np, b) == c["sha256_sorted_i32"]
+    return {"workload": "n=2^16 uniform uint32 (BASELINE config 1)", "cores": 1,
+            "verified": "fixture" if ok else "FIXTURE MISMATCH",
+            "std_sort": {"ms": round(t_std * 1e3, 4), "Mkeys_s": round(n / t_std / 1e6, 2)},
+            "order_with_trust": {"ms": round(t_trust * 1e3, 4), "Mkeys_s": round(n / t_trust / 1e6, 2)},
+            "published_reference": {"std_sort_ms": 2.383, "thrust_host_ms": 0.384,
+                                    "source": "Informe p.5 (BASELINE.md), other host, for context"}}
+
+
+def config1_gpu(ls, torch, dev, stream):
+    """BASELINE config 1's array through the GPU: order_array (the drop-in, host pointer
+    in/out: H2D + sort + D2H, the call main.cpp:28 times) and the device-resident sort;
+    both checked against the committed fixture's SHA-256 (no CPU sort)."""
+    import numpy as np
+    c = _config1_fixture()
+    n = 1 << c["log2n"]
+    src = torch.empty(n, dtype=torch.int32, device=dev)
+    ls.fill(src, n, c["seed"], c["dist"], stream=stream)
+    torch.cuda.synchronize()
+    a = src.cpu().numpy()
+    ok = _sha(np, a) == c["sha256_input"]
+    h = a.copy()
+
+    def oa():
+        np.copyto(h, a)
+        ls.order_array(h)
+    oa()
+    t_oa = _median_s(oa, 50)
+    ok = ok and _sha(np, h) == c["sha256_sorted_i32"]
+    out = torch.empty_like(src)
+    ws = torch.empty(max(ls.workspace_bytes(n, "auto"), 256), dtype=torch.uint8, device=dev)
+    for _ in range(5):
+        ls.sort_device(src, out, n, key="u32", algo="auto", workspace=ws, stream=stream)
+    torch.cuda.synchronize()
+    reps = 200
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ls.sort_device(src, out, n, key="u32", algo="auto", workspace=ws, stream=stream)
+    torch.cuda.synchronize()
+    t_dev = (time.perf_counter() - t0) / reps
+    ok = ok and _sha(np, out.cpu().numpy().view(np.uint32)) == c["sha256_sorted_u32"]
+    return {"workload": "n=2^16 uniform uint32 (BASELINE config 1) through the GPU",
+            "verified": "fixture" if ok else "FIXTURE MISMATCH",
+            "order_array_host_pointer": {"ms": round(t_oa * 1e3, 4), "Mkeys_s": round(n / t_oa / 1e6, 2)},
+            "sort_device": {"ms": round(t_dev * 1e3, 4), "Mkeys_s": round(n / t_dev / 1e6, 2)},
+            "published_reference_order_array_ms": 1.066}
+
+
 def host_fingerprint(np, a):
     """count, sum and sum of squares (mod 2^64) of the keys as uint32, in 64 Mi-key chunks"""
     u = a.view(np.uint32)
@@ -224,6 +312,16 @@ def host_leg_main(args) -> None:
         el, ok = timed(lambda a: ls.sort_host(a, algo="auto"), 3)
         out["single_gpu"] = {"ms": round(el * 1e3, 3), "Mkeys_s": round(n / el / 1e6, 2), "verified": ok,
                              "call": "labsort_sort_host (order_array; pipelined chunks from 2^27 keys)"}
+        # BASELINE config 5's own partition on this GPU: 8 ranks sharing it (peer copies
+        # stand in for xGMI): chunked H2D per rank, splitters, exchange, merge, ranged D2H
+        el, ok = timed(lambda a: ls.sort_host_ranks(a, [0] * 8, transport="peer"), 3)
+        ph, sent = ls.multi_timing()
+        counts = ls.multi_range_counts(8)
+        out["config5_8ranks_one_gpu"] = {
+            "ms": round(el * 1e3, 3), "Mkeys_s": round(n / el / 1e6, 2), "verified": ok,
+            "call": "labsort_sort_host_ranks(devices [0]*8, peer): the 8-rank schedule on one GPU",
+            "phases_ms": {k: round(v, 3) for k, v in ph.items()}, "max_sent_bytes": sent,
+            "max_range_over_share": round(max(counts) / (n / 8), 4)}
     if args.gpus > 1 and torch.cuda.device_count() < args.gpus:
         out[f"error_{args.host_leg}"] = f"{torch.cuda.device_count()} devices visible, {args.gpus} needed"
     elif args.gpus > 1:
@@ -306,17 +404,24 @@ def main():
         else:
             dist.init_process_group("gloo")
         dmod = importlib.import_module(PKG_NAME + ".dist")
-        comm = dmod.P2PComm() if args.backend == "nccl" else dmod.HostStagedComm()
-        ops = dmod.HipOps(ls, key=key, local_algo="radix", stream=stream)
         src = torch.empty(n, dtype=torch.int32, device=dev)
         with torch.cuda.stream(stream):
             ls.fill(src, n, SEED + 5, args.dist, first=rank * n, stream=stream)
+        if args.exchange == "splitters":
+            # the product: labsort_dist_sort (csrc/dist_plan.h's schedule in C++) on this
+            # rank's communicator -- RCCL (ncclCommInitRank) or, backend gloo, host-staged
+            dcomm = dmod.make_comm(ls, backend=args.backend)
 
-        def step():
-            with torch.cuda.stream(stream):
-                if args.exchange == "splitters":
-                    return dmod.dist_sort_splitters(src, ops, copy_input=True, comm=comm)
-                return dmod.dist_sort(src, ops, copy_input=True, comm=comm)
+            def step():
+                ptr, cnt, _ = dcomm.sort(src, n, key=key, stream=stream)
+                return ptr, cnt
+        else:
+            comm = dmod.P2PComm() if args.backend == "nccl" else dmod.HostStagedComm()
+            ops = dmod.HipOps(ls, key=key, local_algo="radix", stream=stream)
+
+            def step():
+                with torch.cuda.stream(stream):
+                    return dmod.dist_sort(src, ops, copy_input=True, comm=comm)
 
         def barrier():
             dist.barrier()
@@ -366,7 +471,7 @@ def main():
         else "merge"
     if args.algo == "radix" and world == 1 and ls.radix_impl(n) == "gather":
         dom = "gsweep"  # the gathered passes (2^16 <= n < 2^26)
-    if world > 1:
+    if world > 1 and args.exchange != "splitters":
         comm.sent_bytes, comm.p2p_rounds, comm.exchange_s = 0, 0, 0.0
         comm.timed = True
     ls.timing_enable(True)
@@ -388,6 +493,9 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+        if args.exchange == "splitters":  # the last step's range, viewed in the comm's buffer
+            res = ls.DistComm.view(*res)
+            dphase, dsent = dcomm.timing()
         # global check: every shard sorted, boundaries ordered, multiset preserved
         nres = res.numel()  # the splitter exchange leaves ranges of slightly different sizes
         cnt = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -511,27 +619,47 @@ def main():
                    "verified": "sorted permutation (descents, digit histograms, sums)"}
         del s2, o2, w2
 
+    config1 = None
+    if world == 1 and args.algo == "radix" and not args.no_merge:
+        config1 = config1_gpu(ls, torch, dev, stream)
+        if config1["verified"] != "fixture":
+            print("bench.py: CONFIG 1 OUTPUT CHECK FAILED", file=sys.stderr)
+            sys.exit(3)
+
     total_keys = n * world * args.steps
     value = total_keys / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
     xgmi = None
     if world > 1:
         import torch.distributed as dist
-        st = torch.tensor([comm.sent_bytes, comm.exchange_s * 1e9, comm.p2p_rounds], dtype=torch.float64,
-                          device=cdev)
+        if args.exchange == "splitters":
+            vals = [float(dsent), dphase["exchange"] * 1e6, 1.0] + [dphase[k] * 1e6 for k in
+                                                                    ("local_sort", "plan", "exchange", "merge")]
+        else:
+            vals = [comm.sent_bytes / args.steps, comm.exchange_s * 1e9 / args.steps, comm.p2p_rounds / args.steps,
+                    0.0, 0.0, 0.0, 0.0]
+        st = torch.tensor(vals, dtype=torch.float64, device=cdev)
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
-        sent, exs, rounds = float(st[0]) / args.steps, float(st[1]) / 1e9 / args.steps, float(st[2]) / args.steps
+        sent, exs, rounds = float(st[0]), float(st[1]) / 1e9, float(st[2])
         links = world - 1 if args.exchange == "splitters" else 1
         xgmi = {"bytes_sent_per_rank_per_step": int(sent), "p2p_rounds_per_step": rounds,
                 "exchange_ms_per_step": round(exs * 1e3, 4),
                 "links_per_round": links,
                 "per_link_GBps": round(sent / links / exs / 1e9, 2) if exs > 0 else None,
-                "note": "max over ranks; exchange time is host wall time around the point-to-point calls "
-                        "(stream synchronised on both sides)"}
+                "note": ("max over ranks, last step; exchange = device time of the grouped ncclSend/ncclRecv "
+                         "(labsort_dist_timing)" if args.exchange == "splitters" else
+                         "max over ranks; exchange time is host wall time around the point-to-point calls "
+                         "(stream synchronised on both sides)")}
+        if args.exchange == "splitters":
+            xgmi["phases_ms_last_step"] = {k: round(float(st[3 + i]) / 1e6, 4) for i, k in
+                                           enumerate(("local_sort", "plan", "exchange", "merge"))}
 
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
+        if args.exchange == "splitters":
+            del res
+            dcomm.close()
         dist.destroy_process_group()
     # the host-pointer leg runs once every rank is done with its GPU
     hostp = host_leg(args) if rank == 0 and not args.no_host_path and args.backend == "nccl" else None
@@ -551,14 +679,15 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds, n, ls)
+            cpu["config1"] = config1_cpu(ls)
         wl = {"radix": "LSD radix sort (8-bit digits, onesweep)", "merge": "LDS tile sort + merge-path passes",
               "radix1": "LSD radix with 1-bit split passes (letra.pdf)",
               "pairs": "stable key/value sort (uint32 key + uint32 index payload): " + (
                   "8-bit LSD onesweep passes" if args.pair_algo == "radix" else "LDS tile sort + merge-path passes")
               }[args.algo]
         if world > 1:
-            how = ("splitter exchange (pairwise send/recv to all peers at once) + one K-way merge of the received runs"
-                   if args.exchange == "splitters" else "bitonic pairwise merge-split network")
+            how = ("splitter exchange (labsort_dist_sort: pairwise ncclSend/ncclRecv to all peers at once, merge of "
+                   "the received runs)" if args.exchange == "splitters" else "bitonic pairwise merge-split network")
             workload = (f"merge sort across {world} GPUs: local radix sort of 2^{args.log2n} uint32 keys per GPU "
                         f"+ {how} over RCCL/xGMI (BASELINE config 5 shape, weak scaling)")
         else:
@@ -578,6 +707,8 @@ def main():
         }
         if merge_leg:
             line["merge"] = merge_leg
+        if config1:
+            line["config1"] = config1
         if config2:
             line["config2"] = config2
         if xgmi:

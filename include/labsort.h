@@ -111,34 +111,79 @@ int labsort_workspace_status(const void *d_workspace, size_t n, int algo, void *
 /* The same for the last labsort_sort_pairs_device(n, algo) on d_workspace. */
 int labsort_pairs_workspace_status(const void *d_workspace, size_t n, int algo, void *stream);
 
-/* ---- one process, several GPUs (the reference is
- * single-GPU, lab.cu:303-402) ----
- * Sort a host buffer in place with nranks ranks: rank r takes the contiguous shard
- * h_keys[r*n/p, (r+1)*n/p) over its own PCIe link (one host thread per rank), sorts it
- * locally (LABSORT_ALGO_AUTO), then the ranks agree on p-1 (key, rank, position)
- * splitters from a regular sample of every sorted shard, cut their shards at them
- * (labsort_upper_bound), exchange piece j -> rank j, merge the p received runs in one
- * K-way pass (labsort_merge_runs) and copy their ranges back to their global offsets.
- * transport: LABSORT_XFER_RCCL (ncclSend/ncclRecv to every peer in one group; one rank
- * per device), LABSORT_XFER_PEER (hipMemcpyPeerAsync; ranks may share a device) or
- * LABSORT_XFER_AUTO (RCCL for distinct devices, peer copies otherwise).  Synchronous.
- * order_array / sort use it when LABSORT_GPUS > 1. */
+/* ---- the merge-sort path across GPUs (the reference
+ * is single-GPU, lab.cu:303-402).  One schedule (csrc/dist_plan.h) for every form:
+ * each rank sorts its shard locally (LABSORT_ALGO_AUTO), the ranks agree on p-1
+ * (key, rank, position) splitters from a regular sample of every sorted shard, cut
+ * their shards at them (labsort_upper_bound), send piece j to rank j by pairwise
+ * send/recv with every peer at once, and merge the p received runs in rank order
+ * (labsort_merge_runs pair passes, then the last level by diagonal ranges).  Rank r
+ * ends with the contiguous range [goff, goff + count) of the sorted array. ----
+ *
+ * One process, several GPUs (one host thread per rank): sort a host buffer in place.
+ * Rank r copies the shard h_keys[r*n/p, (r+1)*n/p) over its own PCIe link in 8 chunks
+ * while earlier chunks sort (from 2^24 keys per rank; LABSORT_HOST_PIPE=0 never, =1
+ * from 2^16), and copies its merged range back to its global offset range by range as
+ * the last merge level lands.  LABSORT_PIN=1 page-locks the caller's array for the
+ * call (hipHostRegister).  transport: LABSORT_XFER_PEER (hipMemcpyPeerAsync into each
+ * receiver's slot; ranks may share a device), LABSORT_XFER_RCCL (ncclSend/ncclRecv
+ * with every peer in one group per rank, communicators from ncclCommInitAll; one rank
+ * per device) or LABSORT_XFER_AUTO (= PEER).  Synchronous.  order_array / sort use
+ * labsort_sort_host_multi when LABSORT_GPUS > 1. */
 #define LABSORT_XFER_AUTO 0
 #define LABSORT_XFER_RCCL 1
 #define LABSORT_XFER_PEER 2
 #define LABSORT_MULTI_MAX_RANKS 8
-/* phases of labsort_multi_timing, ms of the last call (max over ranks where per rank):
- * 0 H2D, 1 local sort, 2 splitters + cut points, 3 exchange, 4 merge, 5 D2H, 6 total */
+/* phases of labsort_multi_timing / labsort_dist_timing, ms of the last call (device
+ * timeline, max over ranks; phases may overlap): 0 H2D (host input), 1 local sort,
+ * 2 samples + splitters + cut points, 3 exchange, 4 merge, 5 D2H tail after the
+ * merge (host output), 6 total (host wall time) */
 #define LABSORT_MULTI_PHASES 7
 int labsort_sort_host_multi(void *h_keys, size_t n, int key_type, int ngpus);  /* devices 0..ngpus-1 */
 int labsort_sort_host_ranks(void *h_keys, size_t n, int key_type, int nranks, const int *devices, int transport);
 int labsort_multi_timing(double *phase_ms, int nphases, size_t *max_sent_bytes);
 int labsort_multi_last_hip_error(void);
+/* keys of each rank's range of the sorted array in the last call (ranks in order) */
+int labsort_multi_range_counts(size_t *counts, int nranks);
+/* text of the last failure of a multi-GPU call (HIP call, RCCL result, callback) */
+const char *labsort_multi_error_detail(void);
 /* The exchange plan alone, on host shards (sorted h_shards[r][0..m[r]) per rank;
  * std::upper_bound stands in for the device bound queries): writes the cut points,
  * h_cuts[r*(nranks+1) + j] = first position of the piece rank r sends to rank j.
  * Test hook for the schedule; no GPU involved. */
 int labsort_multi_plan(const uint32_t *const *h_shards, const size_t *m, int nranks, int key_type, size_t *h_cuts);
+
+/* One process per GPU (torch.distributed.run / mpirun style): a communicator handle
+ * per rank, then one labsort_dist_sort call per rank and sort.
+ *   RCCL: rank 0 calls labsort_comm_unique_id, the id (LABSORT_COMM_ID_BYTES) is
+ *         broadcast by the caller's own means, every rank calls labsort_comm_init_rccl
+ *         with its device current (ncclCommInitRank).
+ *   Host callbacks: the collectives are the caller's (labsort_host_coll over host
+ *         buffers; device pieces are staged): several ranks may share a GPU (tests). */
+#define LABSORT_COMM_ID_BYTES 128
+typedef struct labsort_comm *labsort_comm_t;
+typedef struct {
+    void *ctx;
+    /* h_out[i * bytes .. (i+1) * bytes) = rank i's h_in; return 0 on success */
+    int (*allgather)(void *ctx, const void *h_in, void *h_out, size_t bytes);
+    /* send_bytes[j] bytes of h_send (pieces back to back in rank order) to rank j,
+     * recv_bytes[i] bytes from rank i into h_recv (rank order); own entries are 0 */
+    int (*alltoallv)(void *ctx, const void *h_send, const size_t *send_bytes, void *h_recv,
+                     const size_t *recv_bytes);
+} labsort_host_coll;
+int labsort_comm_unique_id(void *id);
+int labsort_comm_init_rccl(labsort_comm_t *comm, const void *id, int nranks, int rank);
+int labsort_comm_init_host(labsort_comm_t *comm, int nranks, int rank, const labsort_host_coll *coll);
+int labsort_comm_destroy(labsort_comm_t comm);
+/* This rank's shard d_keys[0..m) (device, on the comm's device; left untouched) in;
+ * out: *d_result = this rank's range of the sorted array (*count keys, global offset
+ * *global_offset), in a buffer the communicator owns until its next sort.  Runs on
+ * `stream` (ordered after the work already queued there) and returns once the range
+ * is complete. */
+int labsort_dist_sort(labsort_comm_t comm, const void *d_keys, size_t m, int key_type, void *stream,
+                      const void **d_result, size_t *count, size_t *global_offset);
+int labsort_dist_timing(labsort_comm_t comm, double *phase_ms, int nphases, size_t *sent_bytes);
+int labsort_dist_last_hip_error(labsort_comm_t comm);
 
 /* ---- key/value (sort_by_key; no lab.cu counterpart, the reference sorts
  * keys only) ----

@@ -34,6 +34,15 @@ DIST = {"u32": 0, "u31": 1, "mod100": 2, "mod1000": 3, "sorted": 4, "reversed": 
 
 _lib = None
 
+# labsort_host_coll of include/labsort.h (the same layout as the package's HostColl)
+_AG = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+_A2A = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                        ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t))
+
+
+class _HostColl(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("allgather", _AG), ("alltoallv", _A2A)]
+
 
 def build() -> None:
     subprocess.run(["make", "-s", "-C", HERE], check=True)
@@ -59,6 +68,8 @@ def lib() -> ctypes.CDLL:
         L.labcu_radix_tiles.argtypes = [p, ctypes.c_int]
         L.labcu_warp_scan.argtypes = [p]
         L.labcu_bsearch.argtypes = [p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.oracle_dist_sort.argtypes = [p, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_HostColl),
+                                       p, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
         _lib = L
     return _lib
 
@@ -136,3 +147,40 @@ def time_sort_u32(keys: np.ndarray, threads: int = 1, reps: int = 1) -> float:
     keys = np.ascontiguousarray(keys, dtype=np.uint32)
     scratch = np.empty_like(keys)
     return lib().oracle_time_sort_u32(_ptr(keys), keys.size, threads, reps, _ptr(scratch))
+
+
+def dist_sort(shard: np.ndarray, key: str, world: int, rank: int, coll, cap: int = 0) -> tuple[np.ndarray, int]:
+    """One rank of the PRODUCT's multi-GPU schedule (csrc/dist_plan.h, dist::sort_rank)
+    with host rank operations (std::sort, std::upper_bound, std::merge) over `coll`'s
+    host collectives (world, allgather(h_in, h_out, nbytes), alltoallv(h_send,
+    send_bytes, h_recv, recv_bytes): the package's dist.GlooColl).  Returns this rank's
+    range of the sorted array and its global offset.  cap: room for the range (default
+    twice the shard times the world size; pass the global key count for ragged shards)."""
+    import traceback
+
+    def ag(_c, hi, ho, nb):
+        try:
+            coll.allgather(hi, ho, int(nb))
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    def a2a(_c, hs, sb, hr, rb):
+        try:
+            coll.alltoallv(hs, [int(sb[i]) for i in range(world)], hr, [int(rb[i]) for i in range(world)])
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    hc = _HostColl(None, _AG(ag), _A2A(a2a))
+    a = np.ascontiguousarray(shard).view(np.uint32)
+    cap = cap or 2 * a.size * world + 16
+    out = np.empty(cap, dtype=np.uint32)
+    cnt, goff = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    st = lib().oracle_dist_sort(_ptr(a) if a.size else None, a.size, 1 if key == "i32" else 0, world, rank,
+                                ctypes.byref(hc), _ptr(out), cap, ctypes.byref(cnt), ctypes.byref(goff))
+    if st != 0:
+        raise RuntimeError(f"oracle_dist_sort: status {st}")
+    return out[:cnt.value].copy(), goff.value

@@ -43,7 +43,9 @@ C_SYMBOLS = [
     "labsort_pair_tile_keys", "labsort_pairs_workspace_bytes", "labsort_sort_pairs_device",
     "labsort_workspace_status", "labsort_pairs_workspace_status",
     "labsort_sort_host_multi", "labsort_sort_host_ranks", "labsort_multi_timing", "labsort_multi_last_hip_error",
-    "labsort_multi_plan",
+    "labsort_multi_plan", "labsort_multi_error_detail", "labsort_multi_range_counts",
+    "labsort_comm_unique_id", "labsort_comm_init_rccl", "labsort_comm_init_host", "labsort_comm_destroy",
+    "labsort_dist_sort", "labsort_dist_timing", "labsort_dist_last_hip_error",
 ]
 XFER = {"auto": 0, "rccl": 1, "peer": 2}
 MULTI_PHASES = ["h2d", "local_sort", "plan", "exchange", "merge", "d2h", "total"]
@@ -52,6 +54,43 @@ CXX_SYMBOLS = ["_Z11order_arrayPii", "_Z16order_with_trustPii"]
 
 class LabsortError(RuntimeError):
     pass
+
+
+# labsort_host_coll (include/labsort.h): host collectives supplied by the caller
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t),
+                                ctypes.c_void_p, ctypes.POINTER(ctypes.c_size_t))
+
+
+class HostColl(ctypes.Structure):
+    _fields_ = [("ctx", ctypes.c_void_p), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
+
+
+def host_coll(obj) -> HostColl:
+    """labsort_host_coll whose callbacks call obj.allgather(h_in, h_out, nbytes) and
+    obj.alltoallv(h_send, send_bytes, h_recv, recv_bytes) (raw host addresses and lists
+    of byte counts).  A Python exception in a callback becomes a failed status.  Keep
+    the returned structure alive while the communicator uses it."""
+    import traceback
+
+    def ag(_ctx, h_in, h_out, nbytes):
+        try:
+            obj.allgather(h_in, h_out, int(nbytes))
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    def a2a(_ctx, h_send, sb, h_recv, rb):
+        try:
+            n = obj.world
+            obj.alltoallv(h_send, [int(sb[i]) for i in range(n)], h_recv, [int(rb[i]) for i in range(n)])
+            return 0
+        except Exception:
+            traceback.print_exc()
+            return 1
+
+    return HostColl(None, ALLGATHER_FN(ag), ALLTOALLV_FN(a2a))
 
 
 def _load() -> ctypes.CDLL:
@@ -102,6 +141,16 @@ def _load() -> ctypes.CDLL:
     L.labsort_sort_host_ranks.argtypes = [p, sz, i, i, p, i]
     L.labsort_multi_timing.argtypes = [ctypes.POINTER(ctypes.c_double), i, ctypes.POINTER(sz)]
     L.labsort_multi_plan.argtypes = [ctypes.POINTER(p), ctypes.POINTER(sz), i, i, ctypes.POINTER(sz)]
+    L.labsort_multi_range_counts.argtypes = [ctypes.POINTER(sz), i]
+    L.labsort_multi_error_detail.restype = ctypes.c_char_p
+    L.labsort_multi_error_detail.argtypes = []
+    L.labsort_comm_unique_id.argtypes = [p]
+    L.labsort_comm_init_rccl.argtypes = [ctypes.POINTER(p), p, i, i]
+    L.labsort_comm_init_host.argtypes = [ctypes.POINTER(p), i, i, ctypes.POINTER(HostColl)]
+    L.labsort_comm_destroy.argtypes = [p]
+    L.labsort_dist_sort.argtypes = [p, p, sz, i, p, ctypes.POINTER(p), ctypes.POINTER(sz), ctypes.POINTER(sz)]
+    L.labsort_dist_timing.argtypes = [p, ctypes.POINTER(ctypes.c_double), i, ctypes.POINTER(sz)]
+    L.labsort_dist_last_hip_error.argtypes = [p]
     L.labsort_pairs_workspace_status.argtypes = [p, sz, i, p]
     L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
     L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
@@ -183,10 +232,10 @@ def order_with_trust(a: np.ndarray) -> None:
 
 
 def _check_multi(status: int, what: str) -> None:
-    if status == ERR_HIP:
-        raise LabsortError(f"{what} failed: HIP runtime error: "
-                           + lib.labsort_hip_error_string(lib.labsort_multi_last_hip_error()).decode())
-    _check(status, what)
+    if status != OK:
+        detail = lib.labsort_multi_error_detail().decode()
+        raise LabsortError(f"{what} failed: {lib.labsort_error_string(status).decode()}"
+                           + (f" ({detail})" if detail else ""))
 
 
 def sort_host_multi(a: np.ndarray, ngpus: int) -> None:
@@ -216,6 +265,13 @@ def multi_timing() -> tuple[dict, int]:
     return dict(zip(MULTI_PHASES, list(ms))), sent.value
 
 
+def multi_range_counts(nranks: int) -> list:
+    """Keys of each rank's range of the sorted array in the last multi-GPU host sort."""
+    c = (ctypes.c_size_t * nranks)()
+    _check(lib.labsort_multi_range_counts(c, nranks), "multi_range_counts")
+    return list(c)
+
+
 def multi_plan(shards, key: str = "u32") -> np.ndarray:
     """Cut points of the multi-GPU exchange plan for sorted host shards (test hook):
     cuts[r, j] = first position of the piece rank r sends to rank j (cuts[r, p] = m_r)."""
@@ -226,6 +282,85 @@ def multi_plan(shards, key: str = "u32") -> np.ndarray:
     cuts = (ctypes.c_size_t * (p * (p + 1)))()
     _check(lib.labsort_multi_plan(ptrs, ms, p, KEY[key], cuts), "multi_plan")
     return np.array(list(cuts), dtype=np.int64).reshape(p, p + 1)
+
+
+class DistComm:
+    """One rank's communicator of the distributed merge sort (labsort_comm_t; one
+    process per GPU).  DistComm.rccl(world, rank, uid) over RCCL (uid from
+    DistComm.unique_id() on rank 0, broadcast by the caller), or DistComm.host(world,
+    rank, coll) over host collectives (an object with world, allgather and alltoallv:
+    dist.GlooColl), which lets several ranks share one GPU in the tests."""
+
+    def __init__(self, handle, keep=None):
+        self.h = ctypes.c_void_p(handle)
+        self._keep = keep
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        _check_multi(lib.labsort_comm_unique_id(buf), "labsort_comm_unique_id")
+        return buf.raw
+
+    @classmethod
+    def rccl(cls, world: int, rank: int, uid: bytes) -> "DistComm":
+        h = ctypes.c_void_p(0)
+        ub = ctypes.create_string_buffer(bytes(uid), 128)
+        _check_multi(lib.labsort_comm_init_rccl(ctypes.byref(h), ub, world, rank), "labsort_comm_init_rccl")
+        return cls(h.value)
+
+    @classmethod
+    def host(cls, world: int, rank: int, coll_obj) -> "DistComm":
+        coll = host_coll(coll_obj)
+        h = ctypes.c_void_p(0)
+        _check_multi(lib.labsort_comm_init_host(ctypes.byref(h), world, rank, ctypes.byref(coll)),
+                     "labsort_comm_init_host")
+        return cls(h.value, keep=(coll, coll_obj))
+
+    def sort(self, d_keys, m: int, key: str = "u32", stream=None) -> tuple[int, int, int]:
+        """labsort_dist_sort: (device address, count, global offset) of this rank's range
+        of the sorted array, valid until the next sort on this communicator."""
+        res, cnt, goff = ctypes.c_void_p(0), ctypes.c_size_t(0), ctypes.c_size_t(0)
+        st = lib.labsort_dist_sort(self.h, _ptr(d_keys) if m else None, m, KEY[key], _stream(stream),
+                                   ctypes.byref(res), ctypes.byref(cnt), ctypes.byref(goff))
+        _check_multi(st, "labsort_dist_sort")
+        return res.value or 0, cnt.value, goff.value
+
+    def sort_tensor(self, d_keys, m: int, key: str = "u32", stream=None):
+        """As sort(), with the range as an int32 torch tensor viewing the communicator's
+        buffer (no copy; overwritten by the next sort) and its global offset."""
+        ptr, cnt, goff = self.sort(d_keys, m, key, stream)
+        return self.view(ptr, cnt), goff
+
+    @staticmethod
+    def view(ptr: int, count: int):
+        """int32 torch tensor on the current device viewing `count` keys at device
+        address `ptr` (__cuda_array_interface__; no copy, no ownership)."""
+        import torch
+        if count == 0:
+            return torch.empty(0, dtype=torch.int32, device="cuda")
+
+        class _View:
+            __cuda_array_interface__ = {"shape": (count,), "typestr": "<i4", "data": (ptr, False), "version": 2,
+                                        "strides": None}
+        return torch.as_tensor(_View(), device="cuda")
+
+    def timing(self) -> tuple[dict, int]:
+        ms = (ctypes.c_double * len(MULTI_PHASES))()
+        sent = ctypes.c_size_t(0)
+        _check(lib.labsort_dist_timing(self.h, ms, len(MULTI_PHASES), ctypes.byref(sent)), "dist_timing")
+        return dict(zip(MULTI_PHASES, list(ms))), sent.value
+
+    def close(self) -> None:
+        if self.h.value:
+            _check_multi(lib.labsort_comm_destroy(self.h), "labsort_comm_destroy")
+            self.h = ctypes.c_void_p(0)
+
+    def __del__(self):
+        try:
+            if self.h.value:
+                lib.labsort_comm_destroy(self.h)
+        except Exception:
+            pass
 
 
 def _default_algo() -> int:

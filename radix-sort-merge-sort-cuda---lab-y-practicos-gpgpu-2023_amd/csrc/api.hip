@@ -721,9 +721,15 @@ size_t labsort_pairs_workspace_bytes(size_t n, int algo) {
 }
 
 namespace {
-// 8-bit LSD radix of (key, payload) pairs: histogram, plan, four onesweep passes
-// (k_onesweep<8, ..., KV>: 8 K-pair tiles, decoupled look-back) and the final copy of
-// keys and payloads, with the same buffer plan for both.
+// 8-bit LSD radix of (key, payload) pairs: the keys' segmented histogram and plans,
+// then the persistent onesweep passes carrying each payload with its key
+// (k_onesweep_p<..., KV>), the final copy of keys and payloads under the same buffer
+// plan.  LABSORT_PAIRS_OSP=0: the non-persistent key/value pass (k_onesweep<8, ..., KV>).
+bool pairs_persistent() {
+    const char *e = std::getenv("LABSORT_PAIRS_OSP");
+    return !(e && !std::strcmp(e, "0"));
+}
+
 int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint32_t *vo, size_t n, uint32_t flip,
                      char *ws, hipStream_t s) {
     const RadixLayout L = radix_layout(n, 8);
@@ -739,16 +745,35 @@ int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint3
     uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
     uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
     Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
-    HIP_TRY(launch_zero(ws, L.zero_bytes, s));
-    {
-        TimingScope ts(LABSORT_K_HISTOGRAM, s);
-        HIP_TRY(launch_histogram(ki, n, flip, 8, hist, s));
-    }
-    HIP_TRY(launch_plan(hist, n, 8, ki == ko ? 1 : 0, plan, s));
-    for (int p = 0; p < L.P; ++p) {
-        TimingScope ts(LABSORT_K_ONESWEEP, s);
-        HIP_TRY(launch_onesweep(b, plan, p, 8, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
-                                counters + (size_t)p * OSP_NCTR, err, s, &vb));
+    if (pairs_persistent()) {
+        HIP_TRY(launch_zero(ws, L.off_lookback, s));
+        uint32_t *hps = reinterpret_cast<uint32_t *>(ws + L.off_hps);
+        uint32_t *joint = reinterpret_cast<uint32_t *>(ws + L.off_joint);
+        SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
+        {
+            TimingScope ts(LABSORT_K_HISTOGRAM, s);
+            HIP_TRY(launch_hist_seg(ki, n, flip, hps, joint, s));
+        }
+        HIP_TRY(launch_zero(ws + L.off_lookback, L.zero_bytes - L.off_lookback, s));
+        HIP_TRY(launch_plan8(hps, joint, n, ki == ko ? 1 : 0, plan, sps, hist, s));
+        for (int p = 0; p < L.P; ++p) {
+            if (p > 0) HIP_TRY(launch_segplan(plan, p, n, hist, joint, sps, s));
+            TimingScope ts(LABSORT_K_ONESWEEP, s);
+            HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
+                                      counters + (size_t)p * OSP_NCTR, err, s, &vb));
+        }
+    } else {
+        HIP_TRY(launch_zero(ws, L.zero_bytes, s));
+        {
+            TimingScope ts(LABSORT_K_HISTOGRAM, s);
+            HIP_TRY(launch_histogram(ki, n, flip, 8, hist, s));
+        }
+        HIP_TRY(launch_plan(hist, n, 8, ki == ko ? 1 : 0, plan, s));
+        for (int p = 0; p < L.P; ++p) {
+            TimingScope ts(LABSORT_K_ONESWEEP, s);
+            HIP_TRY(launch_onesweep(b, plan, p, 8, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
+                                    counters + (size_t)p * OSP_NCTR, err, s, &vb));
+        }
     }
     HIP_TRY(launch_final_copy(b, plan, n, s));
     HIP_TRY(launch_final_copy(vb, plan, n, s));

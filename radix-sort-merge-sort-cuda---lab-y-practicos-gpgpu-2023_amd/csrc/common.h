@@ -262,7 +262,8 @@ hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, in
 hipError_t launch_segplan(const Plan *plan, int pass, size_t n, const uint32_t *hist, const uint32_t *joint,
                           SegPlan *segplans, hipStream_t s);
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
-                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s);
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s,
+                             const Bufs *vb = nullptr);
 hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);

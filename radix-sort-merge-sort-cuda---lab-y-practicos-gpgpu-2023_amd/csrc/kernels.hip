@@ -695,18 +695,36 @@ __device__ __forceinline__ void osp_store(uint32_t *p, uint32_t v) {
 }
 __device__ __forceinline__ uint32_t osp_load(const uint32_t *p) { return ld_stream<NT_OSP>(p); }
 
+// LABSORT_OSP_BUF: the pass's key loads and scatter stores go through buffer
+// descriptors (32-bit per-lane offsets instead of 64-bit addresses: fewer VGPRs, so
+// fewer spills whose reloads drain the wave's outstanding stores), and each segment's
+// output bases live in LDS (read once per launch), so A's delta no longer waits on a
+// global load issued behind tile C's prefetched keys.
+#ifndef LABSORT_OSP_BUF
+#define LABSORT_OSP_BUF 1
+#endif
+constexpr bool OSP_BUF = LABSORT_OSP_BUF != 0;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t osp_rsrc(const uint32_t *p, uint32_t n) {
+    const uint64_t a = (uint64_t)p;  // wave-uniform: readfirstlane lets the compiler prove it
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(n * 4u), 0x00020000);
+}
+constexpr int OSP_BUF_NT = (LABSORT_NT_LOADS & NT_OSP) ? 2 : 0;  // aux bit 1 = nt
 
 
-template <bool MATCH>
+
+template <bool MATCH, bool KV = false>
 struct OspSmem {
     static constexpr int R = 256, W = OSP_BLOCK / WAVE, TILE = OSP_TILE;
     uint32_t keys[TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0)];  // padded: see osp_pad
+    uint32_t vals[KV ? TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0) : 1];  // key/value: payloads, reordered alike
     uint32_t wh[W * R];
-    uint64_t match[MATCH ? W * R : 1];
+    uint64_t match[MATCH && !KV ? W * R : 1];
     uint32_t probe[WAVE];
     uint32_t ordered;
     uint32_t hist[R];
     uint32_t delta[R];
+    uint32_t base[OSP_BUF && !KV ? NSEG * R : 1];  // the segments' output bases (SegPlan::base)
     uint32_t start[NSEG + 1];
     uint32_t tpre[NSEG + 1];
     uint32_t wsum[8];
@@ -726,11 +744,20 @@ constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 //                    check fails.
 // HIST_FIRST: tile histogram by LDS atomics before ranking, aggregate published
 // early (else summed from the per-wave rank counters after ranking).
-template <int RANK, bool HIST_FIRST>
+// KV: key/value pairs: each payload (vbufs, selected by the plan
+// like the keys) is loaded with its key, reordered in a second LDS buffer and
+// scattered to its key's destination.  The LDS has no room for the match buffer then
+// (the rank falls back to 8 ballots if the lane-order check fails) nor for the bases
+// table, and the registers none for the next tile's prefetch.
+template <int RANK, bool HIST_FIRST, bool KV = false>
 __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
                                                           uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
-                                                          uint32_t *lookback, uint32_t *counter, uint32_t *err) {
-    using S = OspSmem<RANK != OSP_RANK_BALLOT>;
+                                                          uint32_t *lookback, uint32_t *counter, uint32_t *err,
+                                                          Bufs vbufs) {
+    using S = OspSmem<RANK != OSP_RANK_BALLOT, KV>;
+    constexpr bool PF = OSP_PREFETCH && !KV;  // next tile's keys loaded one iteration ahead
+    constexpr bool LBASE = OSP_BUF && !KV;    // bases table in LDS
+    static_assert(!KV || OSP_BUF, "key/value passes use the buffer-descriptor loads and stores");
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW, LBW2 = OSP_LBW2;
     static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
     __shared__ S sm;
@@ -752,6 +779,11 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     const uint32_t climit = sp->maxt << lbits;
 
     for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) sm.wh[i] = 0u;
+    if constexpr (LBASE)
+        for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += OSP_BLOCK) sm.base[i] = sp->base[i];
+    const __amdgpu_buffer_rsrc_t rin = osp_rsrc(in, n), rout = osp_rsrc(out, n);
+    const __amdgpu_buffer_rsrc_t rvin = osp_rsrc(KV ? vbufs.p[srcsel] : in, n),
+                                 rvout = osp_rsrc(KV ? vbufs.p[plan->dst[pass]] : out, n);
     if (tid <= (uint32_t)NSEG) {
         sm.start[tid] = sp->start[tid];
         sm.tpre[tid] = sp->tpre[tid];
@@ -779,7 +811,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     if (tid == 0) {
         const uint32_t c0 = acquire();
         sm.next = c0;
-        sm.next2 = (OSP_PREFETCH && c0 != OSP_DONE) ? acquire() : OSP_DONE;
+        sm.next2 = (PF && c0 != OSP_DONE) ? acquire() : OSP_DONE;
     }
     if (RANK == OSP_RANK_ATOMIC && wid == 0) {
         const bool ord = lds_lane_ordered(sm.probe, lane);
@@ -795,6 +827,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     // carried state of tile A (slot = look-back slot, lo = slot of its segment's first tile)
     uint32_t slotA = OSP_DONE, loA = 0, segA = 0, nvalidA = 0;
     uint32_t kA[KPT];
+    uint32_t vA[KV ? KPT : 1];  // key/value: A's payloads in scatter order
     uint32_t lwA[LBW];
     uint32_t aggA = 0, dstartA = 0;
     uint32_t *wh = sm.wh + wid * R;
@@ -819,21 +852,61 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         tile_range(c, beg, nv);
         const uint32_t woff = wid * (KPT * WAVE) + lane;
         const uint32_t *src = in + beg + woff;
+        if constexpr (OSP_BUF) {  // out-of-range offsets read 0 (replaced by the sentinel)
+            const uint32_t o = (beg + woff) * 4u;
+            if (nv == (uint32_t)TILE) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) k[j] = __builtin_amdgcn_raw_buffer_load_b32(rin, o + j * WAVE * 4, 0, OSP_BUF_NT);
+            } else {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rin, o + j * WAVE * 4, 0, OSP_BUF_NT);
+                    k[j] = woff + j * WAVE < nv ? v : sentinel;
+                }
+            }
+            return;
+        }
         if (nv == (uint32_t)TILE) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) k[j] = osp_load(src + j * WAVE);
         } else {
+            // past the tile's end: load its last key instead and substitute the sentinel.
+            // The load is kept unconditional (the empty asm uses its value): a
+            // conditional load is speculated by the compiler into a FLAT load of a
+            // select between the key's address and a stack slot holding the sentinel.
+            // FLAT loads complete out of order, so every later use of any load result
+            // then waited vmcnt(0) lgkmcnt(0) -- the look-back window was waited for at
+            // the top of the iteration instead of behind B's rank.
+            uint32_t v[KPT];
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) k[j] = woff + j * WAVE < nv ? osp_load(src + j * WAVE) : sentinel;
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t i = woff + j * WAVE;
+                v[j] = osp_load(in + beg + (i < nv ? i : nv - 1u));
+            }
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                asm volatile("" : "+v"(v[j]));
+                k[j] = woff + j * WAVE < nv ? v[j] : sentinel;
+            }
         }
     };
-    uint32_t kB[KPT], kN[KPT];
-    if (OSP_PREFETCH && cB != OSP_DONE) load_tile(cB, kN);
+    // payloads of tile c, in the keys' layout (key/value passes)
+    auto load_vals = [&](uint32_t c, uint32_t (&v)[KPT]) {
+        uint32_t beg, nv;
+        tile_range(c, beg, nv);
+        const uint32_t o = (beg + wid * (KPT * WAVE) + lane) * 4u;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) v[j] = __builtin_amdgcn_raw_buffer_load_b32(rvin, o + j * WAVE * 4, 0, OSP_BUF_NT);
+    };
+    uint32_t kB[KPT], kN[PF ? KPT : 1];
+    uint32_t vB[KV ? KPT : 1];
+    if constexpr (PF)
+        if (cB != OSP_DONE) load_tile(cB, kN);
 
     for (;;) {
-        if (OSP_PREFETCH) {  // B's keys, loaded one iteration ahead
+        if constexpr (PF) {  // B's keys, loaded one iteration ahead
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) kB[j] = kN[j];
+            for (int j = 0; j < KPT; ++j) kB[j] = kN[j < (PF ? KPT : 1) ? j : 0];
         }
         const bool haveB = cB != OSP_DONE;
         const uint32_t segB = cB & segmask, lB = cB >> segbits;
@@ -849,10 +922,11 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             for (int i = 0; i < LBW; ++i)
                 lwA[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
         }
-        if (OSP_PREFETCH) {
+        if constexpr (PF) {
             if (cC != OSP_DONE) load_tile(cC, kN);
         } else if (haveB) {
             load_tile(cB, kB);
+            if constexpr (KV) load_vals(cB, vB);
         }
         if (HIST_FIRST && haveB) {
 #pragma unroll
@@ -882,7 +956,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                     const uint32_t r = wave_atomic_rank(wh, d, lane);
                     rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
                 } else {
-                    const uint64_t m = RANK != OSP_RANK_BALLOT ? lds_peers(wm + d, lane) : match8(d);
+                    const uint64_t m = (RANK != OSP_RANK_BALLOT && !KV) ? lds_peers(wm + d, lane) : match8(d);
                     const uint32_t pre = mbcnt64(m);
                     const uint32_t old = wh[d];
                     if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
@@ -943,7 +1017,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             }
             OSP_CNT(++lbt_);
             if (slotA > loA) st_agent(lookback + (size_t)slotA * R + tid, LB_INC | (excl + aggA));
-            sm.delta[tid] = sp->base[segA * R + tid] + excl - dstartA;
+            sm.delta[tid] = (LBASE ? sm.base[segA * R + tid] : sp->base[segA * R + tid]) + excl - dstartA;
         }
         OSP_T(2, 3);  // look-back completion of A (waves 0-3)
         __syncthreads();  // (2) delta of A, wave counts and wsum of B
@@ -967,7 +1041,17 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             }
         }
         if (slotA != OSP_DONE) {
-            if (nvalidA == (uint32_t)TILE) {
+            if (OSP_BUF) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) {
+                    const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
+                    const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
+                    // a partial tile's sentinels (i >= nvalidA) go past the array's end: dropped
+                    const uint32_t dst = i < nvalidA ? sm.delta[((key ^ flip) >> shift) & 255u] + i : n;
+                    __builtin_amdgcn_raw_buffer_store_b32(key, rout, dst * 4u, 0, (LABSORT_OSP_NT & 1) ? 2 : 0);
+                    if constexpr (KV) __builtin_amdgcn_raw_buffer_store_b32(vA[j], rvout, dst * 4u, 0, 0);
+                }
+            } else if (nvalidA == (uint32_t)TILE) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
@@ -1003,18 +1087,25 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             sm.hist[tid] = 0u;
             dstartA = ds;
         }
-        if (tid == 0) sm.next = (!OSP_PREFETCH || cC != OSP_DONE) ? acquire() : OSP_DONE;
+        if (tid == 0) sm.next = (!PF || cC != OSP_DONE) ? acquire() : OSP_DONE;
         OSP_T(6, 0);  // wave offsets (waves 0-3), acquisition
         __syncthreads();  // (3) wave offsets of B
         OSP_T(7, 0);
 #pragma unroll
-        for (int j = 0; j < KPT; ++j)
-            sm.keys[osp_pad(wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu))] = kB[j];
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t pos = osp_pad(wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu));
+            sm.keys[pos] = kB[j];
+            if constexpr (KV) sm.vals[pos] = vB[j];
+        }
         __syncthreads();  // (4) B reordered in LDS
         OSP_T(8, 0);  // reorder
         if (!OSP_LDS_SCATTER) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * OSP_BLOCK + tid)];
+        }
+        if constexpr (KV) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) vA[j] = sm.vals[osp_pad(j * OSP_BLOCK + tid)];
         }
         // each wave clears its own counters (no barrier before the next ranking)
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
@@ -1024,7 +1115,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         segA = segB;
         nvalidA = nvalidB;
         aggA = hB;
-        if (OSP_PREFETCH) {
+        if constexpr (PF) {
             cB = cC;
             cC = sm.next;
         } else {
@@ -1603,7 +1694,7 @@ static int cu_count() {
 }
 
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
-                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s) {
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s, const Bufs *vb) {
     const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE + NSEG;
     const size_t want = (size_t)OSP_BLOCKS_PER_CU * cu_count();
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
@@ -1612,13 +1703,18 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
         const char *e = std::getenv("LABSORT_OSP");
         variant = (e && e[0] >= '0' && e[0] <= '2' && e[1]) ? ((e[0] - '0') << 1) | (e[1] == '1') : OSP_DEFAULT_VARIANT;
     }
+    if (vb) {  // key/value: the default variant (lane-ordered atomic rank) only
+        k_onesweep_p<2, false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter,
+                                                             err, *vb);
+        return hipGetLastError();
+    }
     switch (variant) {
-    case 0: k_onesweep_p<0, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
-    case 1: k_onesweep_p<0, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
-    case 2: k_onesweep_p<1, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
-    case 3: k_onesweep_p<1, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
-    case 4: k_onesweep_p<2, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
-    case 5: k_onesweep_p<2, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err); break;
+    case 0: k_onesweep_p<0, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
+    case 1: k_onesweep_p<0, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
+    case 2: k_onesweep_p<1, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
+    case 3: k_onesweep_p<1, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
+    case 4: k_onesweep_p<2, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
+    case 5: k_onesweep_p<2, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

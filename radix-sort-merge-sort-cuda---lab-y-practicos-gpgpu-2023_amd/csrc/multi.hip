@@ -1,24 +1,19 @@
-// multi.hip -- order_array across the GPUs of one node, from one host process
-// (the reference is single-GPU: lab.cu:303-402).
+// multi.hip -- the merge-sort path across GPUs (the
+// reference is single-GPU: lab.cu:303-402).  The schedule itself is dist_plan.h's
+// dist::sort_rank, written once; this file supplies its HIP rank operations and three
+// communicators, and the C-ABI entries that drive them:
 //
-//   labsort_sort_host_multi(h, n, key, p)   ranks 0..p-1 on devices 0..p-1, RCCL
-//   labsort_sort_host_ranks(h, n, key, p, devices, transport)   any rank -> device map
-//
-// Schedule (one call = one completed sort of the caller's host buffer, in place):
-//   1. shard r = h[r*n/p, (r+1)*n/p): H2D over rank r's own PCIe link (one host
-//      thread per rank, so the p links copy at once), local radix/merge sort;
-//   2. a regular sample of every sorted shard -> p-1 splitters, each a
-//      (key, rank, position) triple, so runs of one repeated key are cut between
-//      ranks like any other keys (every range stays near n/p);
-//   3. each rank's cut points at the splitters (labsort_upper_bound on its shard);
-//   4. exchange: piece j of rank i -> rank j, straight into rank j's receive buffer
-//      at its rank-ordered slot: RCCL ncclSend/ncclRecv to all peers in one group
-//      (every xGMI link of a GPU carries data at once) or, for ranks that share a
-//      device, peer copies (hipMemcpyPeerAsync);
-//   5. rank j merges its p received runs in one K-way pass (labsort_merge_runs,
-//      equal keys keep rank order) and copies its range D2H to its global offset.
-// The plan of steps 2-3 is host code shared with labsort_multi_plan, which runs it
-// on host shards (std::upper_bound bound queries) so the CPU tests check it.
+//   labsort_sort_host_multi / labsort_sort_host_ranks   one process, one host thread per
+//       rank (order_array with LABSORT_GPUS=p): rank r copies its shard of the caller's
+//       host array over its own PCIe link in chunks while earlier chunks sort, takes part
+//       in the exchange (in-process peer copies, or RCCL on communicators from
+//       ncclCommInitAll), and copies its merged range back to its global offset in
+//       diagonal ranges as each lands;
+//   labsort_dist_sort on a labsort_comm_t               one process per GPU (bench.py
+//       --gpus N under torch.distributed.run): device-resident shard in, this rank's
+//       range of the sorted array out; RCCL communicator from ncclCommInitRank
+//       (labsort_comm_init_rccl), or host-staged callbacks (labsort_comm_init_host: the
+//       tests run several ranks on one GPU over torch.distributed gloo).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -26,124 +21,62 @@
 
 #include <algorithm>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
 #include "../../include/labsort.h"
 #include "common.h"
+#include "dist_plan.h"
 
 namespace labsort {
 namespace {
 
 // ---------------------------------------------------------------------------------
-// the exchange plan (host only)
+// errors: the HIP code of the failing call (per thread) and a detail message
 // ---------------------------------------------------------------------------------
-struct Splitter {
-    uint32_t ord;   // key ^ flip: monotone in key order
-    uint32_t rank;  // rank whose sample it is
-    uint64_t pos;   // position in that rank's sorted shard
-    uint32_t key;   // the 32-bit word
-};
-
-struct ExPlan {
-    int p = 0;
-    std::vector<size_t> m;         // shard sizes
-    std::vector<size_t> cut;       // [r * (p+1) + j]: first position of piece j on rank r
-    std::vector<size_t> recv_off;  // [j * (p+1) + i]: slot of piece i->j in rank j's receive buffer
-    size_t count(int i, int j) const { return cut[i * (p + 1) + j + 1] - cut[i * (p + 1) + j]; }
-    size_t total(int j) const { return recv_off[j * (p + 1) + p]; }
-    size_t roff(int j, int i) const { return recv_off[j * (p + 1) + i]; }
-};
-
-inline size_t sample_pos(size_t m, size_t s, size_t k) { return k * m / s; }
-inline size_t samples_per_rank(int p) { return (size_t)256 * (size_t)p; }  // ranges within ~m/(256p) keys of n/p
-
-// bound query: out[v] = number of keys of rank r's sorted shard <= values[v] (key order)
-using BoundFn = std::function<int(int r, const std::vector<uint32_t> &values, std::vector<uint32_t> &out)>;
-
-std::vector<Splitter> choose_splitters(int p, const std::vector<size_t> &m,
-                                       const std::vector<std::vector<uint32_t>> &samples, uint32_t flip) {
-    const size_t s = samples_per_rank(p);
-    std::vector<Splitter> pool;
-    pool.reserve(s * p);
-    for (int r = 0; r < p; ++r) {
-        if (!m[r]) continue;  // an empty shard samples nothing
-        for (size_t k = 0; k < s; ++k) {
-            const uint32_t key = samples[r][k];
-            pool.push_back({key ^ flip, (uint32_t)r, (uint64_t)sample_pos(m[r], s, k), key});
-        }
-    }
-    // (key, rank, position) order: a sorted shard's positions are already ascending
-    std::stable_sort(pool.begin(), pool.end(), [](const Splitter &a, const Splitter &b) {
-        return a.ord != b.ord ? a.ord < b.ord : a.rank < b.rank;
-    });
-    std::vector<Splitter> spl(p > 1 ? p - 1 : 0);
-    for (int j = 1; j < p; ++j) spl[j - 1] = pool[(size_t)j * pool.size() / p];
-    return spl;
-}
-
-// bound-query values: the splitter keys, then the key just below each (its lower bound)
-std::vector<uint32_t> plan_values(const std::vector<Splitter> &spl, int p, uint32_t flip) {
-    std::vector<uint32_t> vals(p > 1 ? 2 * (p - 1) : 0);
-    for (int j = 0; j < p - 1; ++j) {
-        vals[j] = spl[j].key;
-        vals[p - 1 + j] = spl[j].ord ? ((spl[j].ord - 1) ^ flip) : spl[j].key;
-    }
-    return vals;
-}
-
-int make_plan(ExPlan &P, const std::vector<Splitter> &spl, uint32_t flip, const BoundFn &ub) {
-    const int p = P.p;
-    P.cut.assign((size_t)p * (p + 1), 0);
-    P.recv_off.assign((size_t)p * (p + 1), 0);
-    const std::vector<uint32_t> vals = plan_values(spl, p, flip);
-    std::vector<uint32_t> out;
-    for (int r = 0; r < p; ++r) {
-        size_t *c = &P.cut[(size_t)r * (p + 1)];
-        c[p] = P.m[r];
-        if (!P.m[r] || p == 1) continue;
-        out.assign(vals.size(), 0);
-        const int st = ub(r, vals, out);
-        if (st) return st;
-        for (int j = 0; j < p - 1; ++j) {
-            const size_t upper = out[j], lower = spl[j].ord ? out[p - 1 + j] : 0;
-            size_t x;
-            if (spl[j].rank > (uint32_t)r) x = upper;       // rank r's equal keys precede the splitter
-            else if (spl[j].rank < (uint32_t)r) x = lower;  // ... or follow it
-            else x = (size_t)spl[j].pos + 1;                // the splitter itself ends piece j
-            if (x < c[j] || x > P.m[r]) return LABSORT_ERR_DEVICE;  // inconsistent bounds
-            c[j + 1] = x;
-        }
-    }
-    for (int j = 0; j < p; ++j) {
-        size_t *o = &P.recv_off[(size_t)j * (p + 1)];
-        for (int i = 0; i < p; ++i) o[i + 1] = o[i] + P.count(i, j);
-    }
-    return LABSORT_OK;
-}
-
-// ---------------------------------------------------------------------------------
-// device side
-// ---------------------------------------------------------------------------------
-__global__ void k_sample(const uint32_t *__restrict__ keys, uint64_t m, uint32_t s, uint32_t *__restrict__ out) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < s) out[k] = keys[(uint64_t)k * m / s];
-}
-
 thread_local int t_last_hip = 0;
-#define MHIP(x)                                  \
-    do {                                         \
-        hipError_t _e = (x);                     \
-        if (_e != hipSuccess) {                  \
-            t_last_hip = (int)_e;                \
-            return LABSORT_ERR_HIP;              \
-        }                                        \
+std::mutex g_err_mu;
+std::string g_detail;  // last failure of a multi-GPU call, human readable
+
+void set_detail(const std::string &s) {
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    g_detail = s;
+}
+
+#define MHIP(x)                                                                                    \
+    do {                                                                                           \
+        hipError_t _e = (x);                                                                       \
+        if (_e != hipSuccess) {                                                                    \
+            t_last_hip = (int)_e;                                                                  \
+            set_detail(std::string(#x) + ": " + hipGetErrorString(_e));                            \
+            return LABSORT_ERR_HIP;                                                                \
+        }                                                                                          \
     } while (0)
+// a labsort_* call: an ERR_HIP it returns recorded its code in api.hip's thread-local slot
+#define LCALL(x)                                                                                   \
+    do {                                                                                           \
+        const int _s = (x);                                                                        \
+        if (_s != LABSORT_OK) {                                                                    \
+            if (_s == LABSORT_ERR_HIP) {                                                           \
+                t_last_hip = labsort_last_hip_error();                                             \
+                set_detail(std::string(#x) + ": " + hipGetErrorString((hipError_t)t_last_hip));    \
+            } else {                                                                               \
+                set_detail(std::string(#x) + ": " + labsort_error_string(_s));                     \
+            }                                                                                      \
+            return _s;                                                                             \
+        }                                                                                          \
+    } while (0)
+
+double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct Buf {
     void *p = nullptr;
@@ -159,146 +92,507 @@ int grow(Buf &b, size_t need) {
     b.bytes = want;
     return LABSORT_OK;
 }
+template <class T>
+T *as(Buf &b) {
+    return static_cast<T *>(b.p);
+}
+
+__global__ void k_sample(const uint32_t *__restrict__ keys, uint64_t m, uint32_t s, uint32_t *__restrict__ out) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < s) out[k] = keys[(uint64_t)k * m / s];  // = dist::sample_pos (k * m < 2^42)
+}
+
+// ---------------------------------------------------------------------------------
+// one rank's device state (persistent across calls) and its HIP operations
+// ---------------------------------------------------------------------------------
+constexpr int RANK_CHUNKS = 8;   // host input: shard copied and sorted in chunks
+constexpr int RANK_RANGES = 8;   // host output: the last merge level in diagonal ranges, D2H per range
+constexpr size_t RANK_PIPE_MIN = (size_t)1 << 24;  // keys per rank from which the host input is chunked
+
+// LABSORT_HOST_PIPE: "0" never chunk, "1" from 2^16 keys per rank (tests), unset RANK_PIPE_MIN
+size_t rank_pipe_min() {
+    const char *e = std::getenv("LABSORT_HOST_PIPE");
+    if (e && !std::strcmp(e, "0")) return ~(size_t)0;
+    if (e && !std::strcmp(e, "1")) return (size_t)1 << 16;
+    return RANK_PIPE_MIN;
+}
+
+enum { EV_H2D = dist::M_NMARKS, EV_D2H, EV_NEV };
 
 struct RankState {
     int dev = -1;
-    hipStream_t s = nullptr;
-    hipEvent_t ev = nullptr;
-    Buf keys, recv, out, ws, kmws, small;
+    hipStream_t own = nullptr, copy = nullptr;  // own compute stream (in-process ranks), copy stream
+    hipEvent_t chunk_ev[RANK_CHUNKS] = {}, range_ev[RANK_RANGES] = {};
+    hipEvent_t tev[EV_NEV] = {};  // timing: schedule marks, end of H2D, end of D2H
+    Buf x, y, ws, mws, recv, out, small, part, errs;
+    int nerrs = 0;
 };
 
+int bind_rank(RankState &R, int dev) {
+    if (R.dev == dev && R.own) return LABSORT_OK;
+    if (R.dev >= 0) {  // device changed: drop the old buffers on their device
+        MHIP(hipSetDevice(R.dev));
+        for (Buf *b : {&R.x, &R.y, &R.ws, &R.mws, &R.recv, &R.out, &R.small, &R.part, &R.errs})
+            if (b->p) MHIP(hipFree(b->p));
+        for (hipStream_t s : {R.own, R.copy})
+            if (s) MHIP(hipStreamDestroy(s));
+        for (hipEvent_t e : R.chunk_ev)
+            if (e) MHIP(hipEventDestroy(e));
+        for (hipEvent_t e : R.range_ev)
+            if (e) MHIP(hipEventDestroy(e));
+        for (hipEvent_t e : R.tev)
+            if (e) MHIP(hipEventDestroy(e));
+        R = RankState{};
+    }
+    MHIP(hipSetDevice(dev));
+    MHIP(hipStreamCreateWithFlags(&R.own, hipStreamNonBlocking));
+    MHIP(hipStreamCreateWithFlags(&R.copy, hipStreamNonBlocking));
+    for (hipEvent_t &e : R.chunk_ev) MHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t &e : R.range_ev) MHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    for (hipEvent_t &e : R.tev) MHIP(hipEventCreate(&e));
+    R.dev = dev;
+    return LABSORT_OK;
+}
+
+// dist::sort_rank's Ops on one GPU.  host_in: `in` is a host address (the caller's
+// array); otherwise a device address.
+struct HipRankOps {
+    RankState &R;
+    hipStream_t s;
+    int key_type;
+    bool host_in;
+    uint32_t flip() const { return key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u; }
+
+    void mark(dist::Mark k) { (void)hipEventRecord(R.tev[k], s); }
+
+    // sort one piece in -> out (device) with the workspace; its radix error word copied aside
+    int sort_piece(const uint32_t *in, uint32_t *out, size_t len) {
+        const int algo = LABSORT_ALGO_AUTO;
+        LCALL(labsort_sort_device(in, out, len, key_type, algo, R.ws.p, R.ws.bytes, s));
+        // AUTO ran a radix layout (its first word is the device error word)
+        if (R.nerrs < RANK_CHUNKS && len > (size_t)LABSORT_AUTO_MERGE_MAX_KEYS && len <= labsort_max_keys(LABSORT_ALGO_RADIX))
+            MHIP(hipMemcpyAsync(as<uint32_t>(R.errs) + R.nerrs++, R.ws.p, 4, hipMemcpyDeviceToDevice, s));
+        return LABSORT_OK;
+    }
+
+    int local_sort(const uint32_t *in, uint64_t m, const uint32_t **sorted) {
+        int st;
+        R.nerrs = 0;
+        if ((st = grow(R.errs, RANK_CHUNKS * 4))) return st;
+        MHIP(hipMemsetAsync(R.errs.p, 0, RANK_CHUNKS * 4, s));
+        if ((st = grow(R.x, m * 4)) || (st = grow(R.y, m * 4))) return st;
+        uint32_t *X = as<uint32_t>(R.x), *Y = as<uint32_t>(R.y);
+        if (!m) {
+            *sorted = X;
+            if (host_in) MHIP(hipEventRecord(R.tev[EV_H2D], s));
+            return LABSORT_OK;
+        }
+        if (!host_in) {  // device-resident shard: one sort into X
+            if ((st = grow(R.ws, labsort_workspace_bytes(m, LABSORT_ALGO_AUTO)))) return st;
+            if ((st = sort_piece(in, X, m))) return st;
+            *sorted = X;
+            return LABSORT_OK;
+        }
+        // host shard: chunk i copied H2D into X on the copy stream while the compute stream
+        // sorts the chunks that have landed (X -> Y); then the chunk runs merged Y -> X
+        const int K = m >= rank_pipe_min() ? RANK_CHUNKS : 1;
+        const size_t c = (m + K - 1) / K;
+        if ((st = grow(R.ws, labsort_workspace_bytes(c, LABSORT_ALGO_AUTO)))) return st;
+        MHIP(hipEventRecord(R.tev[dist::M_START], s));  // the copy stream starts after the zeroed error words
+        MHIP(hipStreamWaitEvent(R.copy, R.tev[dist::M_START], 0));
+        size_t off[RANK_CHUNKS + 1];
+        int nr = 0;
+        for (int i = 0; i < K; ++i) {
+            const size_t o = (size_t)i * c;
+            if (o >= m) break;
+            const size_t len = std::min(c, (size_t)m - o);
+            off[nr++] = o;
+            MHIP(hipMemcpyAsync(X + o, in + o, len * 4, hipMemcpyHostToDevice, R.copy));
+            MHIP(hipEventRecord(R.chunk_ev[i], R.copy));
+            MHIP(hipStreamWaitEvent(s, R.chunk_ev[i], 0));
+            if ((st = sort_piece(X + o, (nr == 1 && K == 1) ? X + o : Y + o, len))) return st;
+        }
+        MHIP(hipEventRecord(R.tev[EV_H2D], R.copy));
+        off[nr] = m;
+        if (nr == 1 && K == 1) {
+            *sorted = X;
+            return LABSORT_OK;
+        }
+        if ((st = grow(R.mws, labsort_merge_runs_workspace_bytes(m)))) return st;
+        LCALL(labsort_merge_runs(Y, X, off, nr, key_type, R.mws.p, R.mws.bytes, s));
+        *sorted = X;
+        return LABSORT_OK;
+    }
+
+    int sample(const uint32_t *S, uint64_t m, size_t n, uint32_t *h_out) {
+        int st;
+        if ((st = grow(R.small, std::max(n, (size_t)4096) * 4))) return st;
+        k_sample<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(S, m, (uint32_t)n, as<uint32_t>(R.small));
+        MHIP(hipGetLastError());
+        MHIP(hipMemcpyAsync(h_out, R.small.p, n * 4, hipMemcpyDeviceToHost, s));
+        MHIP(hipStreamSynchronize(s));
+        return LABSORT_OK;
+    }
+
+    int bounds(const uint32_t *S, uint64_t m, const uint32_t *h_vals, size_t nv, uint32_t *h_out) {
+        int st;
+        if (!nv) return LABSORT_OK;
+        if ((st = grow(R.small, std::max(2 * nv, (size_t)4096) * 4))) return st;
+        uint32_t *d = as<uint32_t>(R.small);
+        MHIP(hipMemcpyAsync(d, h_vals, nv * 4, hipMemcpyHostToDevice, s));
+        LCALL(labsort_upper_bound(S, m, key_type, d, nv, d + nv, s));
+        MHIP(hipMemcpyAsync(h_out, d + nv, nv * 4, hipMemcpyDeviceToHost, s));
+        MHIP(hipStreamSynchronize(s));
+        return LABSORT_OK;
+    }
+
+    int recv_buffer(uint64_t total, uint32_t **recv) {
+        int st;
+        if ((st = grow(R.recv, total * 4)) || (st = grow(R.out, total * 4)) ||
+            (st = grow(R.mws, labsort_merge_runs_workspace_bytes(total))) ||
+            (st = grow(R.part, labsort_merge_parts((total + RANK_RANGES - 1) / RANK_RANGES) * 4)))
+            return st;
+        *recv = as<uint32_t>(R.recv);
+        return LABSORT_OK;
+    }
+
+    int copy_local(uint32_t *dst, const uint32_t *src, uint64_t count) {
+        MHIP(hipMemcpyAsync(dst, src, count * 4, hipMemcpyDeviceToDevice, s));
+        return LABSORT_OK;
+    }
+
+    int to_host(const uint32_t *src, uint64_t count, uint32_t *h_dst) {
+        MHIP(hipEventRecord(R.range_ev[0], s));
+        MHIP(hipStreamWaitEvent(R.copy, R.range_ev[0], 0));
+        MHIP(hipMemcpyAsync(h_dst, src, count * 4, hipMemcpyDeviceToHost, R.copy));
+        MHIP(hipEventRecord(R.tev[EV_D2H], R.copy));
+        return LABSORT_OK;
+    }
+
+    // the p received runs (rank order) merged: the first and second halves of the runs
+    // by labsort_merge_runs (pair passes) into `out`, then the two halves merged back
+    // into `recv` as RANK_RANGES diagonal ranges, each range's D2H (h_sink) on the copy
+    // stream as soon as it lands
+    int merge(const uint32_t *Rv, const uint64_t *offs, int p, uint32_t *h_sink, const uint32_t **result) {
+        const size_t total = offs[p];
+        uint32_t *recv = const_cast<uint32_t *>(Rv), *O = as<uint32_t>(R.out);
+        if (p == 1 || total == 0) {
+            *result = recv;
+            return h_sink && total ? to_host(recv, total, h_sink) : LABSORT_OK;
+        }
+        const int h = (p + 1) / 2;
+        auto half = [&](int q0, int q1) -> int {  // runs [q0, q1) -> O
+            const size_t b = offs[q0], e = offs[q1];
+            if (e == b) return LABSORT_OK;
+            if (q1 - q0 == 1) {
+                MHIP(hipMemcpyAsync(O + b, recv + b, (e - b) * 4, hipMemcpyDeviceToDevice, s));
+                return LABSORT_OK;
+            }
+            size_t o[LABSORT_MULTI_MAX_RANKS + 1];
+            for (int q = q0; q <= q1; ++q) o[q - q0] = offs[q];
+            LCALL(labsort_merge_runs(recv, O, o, q1 - q0, key_type, R.mws.p, R.mws.bytes, s));
+            return LABSORT_OK;
+        };
+        int st;
+        if ((st = half(0, h)) || (st = half(h, p))) return st;
+        const size_t la = offs[h], lb = total - la, rl = (total + RANK_RANGES - 1) / RANK_RANGES;
+        for (int q = 0; q < RANK_RANGES; ++q) {
+            const size_t d0 = (size_t)q * rl, d1 = std::min(total, d0 + rl);
+            if (d0 >= d1) break;
+            LCALL(labsort_merge(O, la, O + la, lb, recv + d0, d0, d1, key_type, as<uint32_t>(R.part), s));
+            if (h_sink) {
+                MHIP(hipEventRecord(R.range_ev[q], s));
+                MHIP(hipStreamWaitEvent(R.copy, R.range_ev[q], 0));
+                MHIP(hipMemcpyAsync(h_sink + d0, recv + d0, (d1 - d0) * 4, hipMemcpyDeviceToHost, R.copy));
+            }
+        }
+        if (h_sink) MHIP(hipEventRecord(R.tev[EV_D2H], R.copy));
+        *result = recv;
+        return LABSORT_OK;
+    }
+
+    // after the schedule: wait for both streams, then the sorts' device error words
+    int finish() {
+        MHIP(hipStreamSynchronize(s));
+        MHIP(hipStreamSynchronize(R.copy));
+        if (R.nerrs) {
+            uint32_t e[RANK_CHUNKS] = {};
+            MHIP(hipMemcpy(e, R.errs.p, R.nerrs * 4, hipMemcpyDeviceToHost));
+            for (int i = 0; i < R.nerrs; ++i)
+                if (e[i]) {
+                    set_detail("a sort kernel reported a device-side error (look-back spin limit)");
+                    return LABSORT_ERR_DEVICE;
+                }
+        }
+        return LABSORT_OK;
+    }
+
+    // phases (ms, device timeline) of the call just finished
+    void phases(double *ph, bool host) {
+        auto el = [&](hipEvent_t a, hipEvent_t b) {
+            float ms = 0.f;
+            return hipEventElapsedTime(&ms, a, b) == hipSuccess ? (double)ms : 0.0;
+        };
+        ph[0] = host ? el(R.tev[dist::M_START], R.tev[EV_H2D]) : 0.0;
+        ph[1] = el(R.tev[dist::M_START], R.tev[dist::M_SORTED]);
+        ph[2] = el(R.tev[dist::M_SORTED], R.tev[dist::M_PLANNED]);
+        ph[3] = el(R.tev[dist::M_PLANNED], R.tev[dist::M_EXCHANGED]);
+        ph[4] = el(R.tev[dist::M_EXCHANGED], R.tev[dist::M_MERGED]);
+        ph[5] = host ? el(R.tev[dist::M_MERGED], R.tev[EV_D2H]) : 0.0;
+    }
+};
+
+// ---------------------------------------------------------------------------------
 // RCCL, loaded on first use (no link-time dependency; in a torch process the
 // already-loaded librccl.so.1 is the one dlopen returns)
+// ---------------------------------------------------------------------------------
 struct Rccl {
     bool tried = false;
     void *h = nullptr;
-    decltype(&ncclCommInitAll) init = nullptr;
+    decltype(&ncclGetUniqueId) uid = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllGather) allgather = nullptr;
     decltype(&ncclSend) send = nullptr;
     decltype(&ncclRecv) recv = nullptr;
     decltype(&ncclGroupStart) gstart = nullptr;
     decltype(&ncclGroupEnd) gend = nullptr;
     decltype(&ncclGetErrorString) errstr = nullptr;
-    std::vector<int> devs;
-    std::vector<ncclComm_t> comms;
     bool load() {
+        static std::mutex mu;
+        std::lock_guard<std::mutex> lk(mu);
         if (tried) return h != nullptr;
         tried = true;
         h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
         if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) return false;
-        init = (decltype(init))dlsym(h, "ncclCommInitAll");
+        if (!h) {
+            set_detail("RCCL: librccl.so could not be loaded");
+            return false;
+        }
+        uid = (decltype(uid))dlsym(h, "ncclGetUniqueId");
+        init_rank = (decltype(init_rank))dlsym(h, "ncclCommInitRank");
+        init_all = (decltype(init_all))dlsym(h, "ncclCommInitAll");
+        destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
+        allgather = (decltype(allgather))dlsym(h, "ncclAllGather");
         send = (decltype(send))dlsym(h, "ncclSend");
         recv = (decltype(recv))dlsym(h, "ncclRecv");
         gstart = (decltype(gstart))dlsym(h, "ncclGroupStart");
         gend = (decltype(gend))dlsym(h, "ncclGroupEnd");
         errstr = (decltype(errstr))dlsym(h, "ncclGetErrorString");
-        if (!init || !send || !recv || !gstart || !gend) h = nullptr;
+        if (!uid || !init_rank || !init_all || !destroy || !allgather || !send || !recv || !gstart || !gend) {
+            set_detail("RCCL: a symbol is missing from librccl.so");
+            h = nullptr;
+        }
         return h != nullptr;
+    }
+    // record an ncclResult as the call's failure detail
+    int fail(const char *what, ncclResult_t r) {
+        set_detail(std::string("RCCL ") + what + ": " + (errstr ? errstr(r) : "error") + " (ncclResult " +
+                   std::to_string((int)r) + ")");
+        t_last_hip = 0;
+        return LABSORT_ERR_HIP;
+    }
+};
+Rccl g_rccl;
+
+#define NCHK(what, x)                                        \
+    do {                                                     \
+        const ncclResult_t _r = (x);                         \
+        if (_r != ncclSuccess) return g_rccl.fail(what, _r); \
+    } while (0)
+
+// grouped pairwise send/recv with every peer at once: every xGMI link of the GPU
+// carries data together (the "pairwise RCCL send/recv merge" of the north_star)
+int rccl_exchange(ncclComm_t c, int p, int me, hipStream_t s, const uint32_t *const *send, const uint64_t *sc,
+                  uint32_t *const *recv, const uint64_t *rc) {
+    NCHK("ncclGroupStart", g_rccl.gstart());
+    ncclResult_t bad = ncclSuccess;
+    for (int j = 0; j < p && bad == ncclSuccess; ++j) {
+        if (j == me) continue;
+        if (sc[j]) bad = g_rccl.send(send[j], sc[j], ncclUint32, j, c, s);
+        if (bad == ncclSuccess && rc[j]) bad = g_rccl.recv(recv[j], rc[j], ncclUint32, j, c, s);
+    }
+    const ncclResult_t e = g_rccl.gend();
+    if (bad != ncclSuccess) return g_rccl.fail("ncclSend/ncclRecv", bad);
+    if (e != ncclSuccess) return g_rccl.fail("ncclGroupEnd", e);
+    return LABSORT_OK;
+}
+
+// ---------------------------------------------------------------------------------
+// communicator 1: in-process ranks (one host thread each)
+// ---------------------------------------------------------------------------------
+struct ThreadShared {
+    int p = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    unsigned gen = 0;
+    bool failed = false;
+    std::vector<std::vector<uint8_t>> slot;
+    std::vector<uint32_t *const *> rptr;  // each rank's receive addresses (during an exchange)
+    std::vector<hipEvent_t> sent;          // each rank's "my sends are queued" event
+    std::vector<int> dev;
+    std::vector<ncclComm_t> comms;         // RCCL transport: one communicator per rank
+    explicit ThreadShared(int n) : p(n), slot(n), rptr(n, nullptr), sent(n, nullptr), dev(n, -1) {}
+
+    // all ranks arrive; LABSORT_ERR_DEVICE if one of them failed (it never arrives)
+    int barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (failed) return LABSORT_ERR_DEVICE;
+        const unsigned g = gen;
+        if (++arrived == p) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return LABSORT_OK;
+        }
+        cv.wait(lk, [&] { return gen != g || failed; });
+        return gen != g ? LABSORT_OK : LABSORT_ERR_DEVICE;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu);
+        failed = true;
+        cv.notify_all();
     }
 };
 
-std::mutex g_mu;                 // one multi-GPU sort at a time
+struct ThreadComm {
+    ThreadShared &sh;
+    int me;
+    hipStream_t s;
+    bool rccl;
+    int size() const { return sh.p; }
+    int rank() const { return me; }
+    int allgather(const void *in, void *out, size_t bytes) {
+        int st;
+        sh.slot[me].assign(static_cast<const uint8_t *>(in), static_cast<const uint8_t *>(in) + bytes);
+        if ((st = sh.barrier())) return st;
+        for (int i = 0; i < sh.p; ++i) {
+            if (sh.slot[i].size() != bytes) return LABSORT_ERR_ARG;
+            memcpy(static_cast<uint8_t *>(out) + (size_t)i * bytes, sh.slot[i].data(), bytes);
+        }
+        return sh.barrier();  // every rank has read every slot
+    }
+    int exchange(const uint32_t *const *send, const uint64_t *sc, uint32_t *const *recv, const uint64_t *rc) {
+        int st;
+        if (rccl) return rccl_exchange(sh.comms[me], sh.p, me, s, send, sc, recv, rc);
+        // peer copies straight into each receiver's slot, on the sender's stream; the
+        // receivers' streams then wait for every sender's event
+        sh.rptr[me] = recv;
+        if ((st = sh.barrier())) return st;
+        for (int j = 0; j < sh.p; ++j) {
+            if (j == me || !sc[j]) continue;
+            MHIP(hipMemcpyPeerAsync(sh.rptr[j][me], sh.dev[j], send[j], sh.dev[me], sc[j] * 4, s));
+        }
+        MHIP(hipEventRecord(sh.sent[me], s));
+        if ((st = sh.barrier())) return st;
+        for (int i = 0; i < sh.p; ++i)
+            if (i != me && rc[i]) MHIP(hipStreamWaitEvent(s, sh.sent[i], 0));
+        return sh.barrier();  // the receive addresses are no longer read
+    }
+};
+
+// ---------------------------------------------------------------------------------
+// communicator 2: one process per rank over RCCL (ncclCommInitRank)
+// communicator 3: host-staged callbacks (tests: torch.distributed gloo)
+// ---------------------------------------------------------------------------------
+struct RcclComm {
+    ncclComm_t c;
+    int p, me;
+    hipStream_t s;
+    Buf &stage;
+    int size() const { return p; }
+    int rank() const { return me; }
+    int allgather(const void *in, void *out, size_t bytes) {
+        int st;
+        if ((st = grow(stage, bytes * (p + 1)))) return st;
+        uint8_t *d = as<uint8_t>(stage);
+        MHIP(hipMemcpyAsync(d + bytes * p, in, bytes, hipMemcpyHostToDevice, s));
+        NCHK("ncclAllGather", g_rccl.allgather(d + bytes * p, d, bytes, ncclUint8, c, s));
+        MHIP(hipMemcpyAsync(out, d, bytes * p, hipMemcpyDeviceToHost, s));
+        MHIP(hipStreamSynchronize(s));
+        return LABSORT_OK;
+    }
+    int exchange(const uint32_t *const *send, const uint64_t *sc, uint32_t *const *recv, const uint64_t *rc) {
+        return rccl_exchange(c, p, me, s, send, sc, recv, rc);
+    }
+};
+
+struct HostCbComm {
+    labsort_host_coll cb;
+    int p, me;
+    hipStream_t s;
+    std::vector<uint32_t> &hs, &hr;  // host staging of the key pieces
+    int size() const { return p; }
+    int rank() const { return me; }
+    int allgather(const void *in, void *out, size_t bytes) {
+        if (cb.allgather(cb.ctx, in, out, bytes)) {
+            set_detail("labsort_host_coll.allgather failed");
+            return LABSORT_ERR_ARG;
+        }
+        return LABSORT_OK;
+    }
+    int exchange(const uint32_t *const *send, const uint64_t *sc, uint32_t *const *recv, const uint64_t *rc) {
+        std::vector<size_t> sb(p), rb(p);
+        size_t ts = 0, tr = 0;
+        for (int j = 0; j < p; ++j) {
+            sb[j] = j == me ? 0 : sc[j] * 4;
+            rb[j] = j == me ? 0 : rc[j] * 4;
+            ts += sb[j] / 4;
+            tr += rb[j] / 4;
+        }
+        hs.resize(std::max<size_t>(ts, 1));
+        hr.resize(std::max<size_t>(tr, 1));
+        size_t o = 0;
+        for (int j = 0; j < p; ++j) {
+            if (sb[j]) MHIP(hipMemcpyAsync(hs.data() + o, send[j], sb[j], hipMemcpyDeviceToHost, s));
+            o += sb[j] / 4;
+        }
+        MHIP(hipStreamSynchronize(s));
+        if (cb.alltoallv(cb.ctx, hs.data(), sb.data(), hr.data(), rb.data())) {
+            set_detail("labsort_host_coll.alltoallv failed");
+            return LABSORT_ERR_ARG;
+        }
+        o = 0;
+        for (int j = 0; j < p; ++j) {
+            if (rb[j]) MHIP(hipMemcpyAsync(recv[j], hr.data() + o, rb[j], hipMemcpyHostToDevice, s));
+            o += rb[j] / 4;
+        }
+        MHIP(hipStreamSynchronize(s));  // the staging buffer may be reused
+        return LABSORT_OK;
+    }
+};
+
+// ---------------------------------------------------------------------------------
+// in-process ranks: labsort_sort_host_ranks
+// ---------------------------------------------------------------------------------
+std::mutex g_mu;                 // one in-process multi-GPU sort at a time
 std::vector<RankState> g_ranks;  // per rank slot, re-bound when its device changes
-Rccl g_rccl;
+std::vector<int> g_comm_devs;    // devices of the cached ncclCommInitAll communicators
+std::vector<ncclComm_t> g_comms;
 double g_phase_ms[LABSORT_MULTI_PHASES];
 size_t g_sent_bytes = 0;
+std::vector<size_t> g_range_counts;  // keys of each rank's range in the last call
 
-double now_ms() {
-    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
-
-int bind_rank(RankState &R, int dev) {
-    if (R.dev == dev && R.s) return LABSORT_OK;
-    if (R.dev >= 0) {  // device changed: drop the old buffers on their device
-        MHIP(hipSetDevice(R.dev));
-        for (Buf *b : {&R.keys, &R.recv, &R.out, &R.ws, &R.kmws, &R.small})
-            if (b->p) MHIP(hipFree(b->p));
-        if (R.s) MHIP(hipStreamDestroy(R.s));
-        if (R.ev) MHIP(hipEventDestroy(R.ev));
-        R = RankState{};
-    }
-    MHIP(hipSetDevice(dev));
-    MHIP(hipStreamCreateWithFlags(&R.s, hipStreamNonBlocking));
-    MHIP(hipEventCreateWithFlags(&R.ev, hipEventDisableTiming));
-    R.dev = dev;
+int rccl_comms(const std::vector<int> &devs) {
+    if (!g_rccl.load()) return LABSORT_ERR_HIP;
+    if (g_comm_devs == devs) return LABSORT_OK;
+    for (ncclComm_t c : g_comms)  // the device set changed: release the old communicators
+        if (c) (void)g_rccl.destroy(c);
+    g_comms.assign(devs.size(), nullptr);
+    g_comm_devs.clear();
+    NCHK("ncclCommInitAll", g_rccl.init_all(g_comms.data(), (int)devs.size(), devs.data()));
+    g_comm_devs = devs;
     return LABSORT_OK;
 }
 
-// run f(r) for every rank on its own host thread (each binds its rank's device)
-int for_ranks(int p, const std::function<int(int)> &f) {
-    std::vector<int> st(p, LABSORT_OK);
-    std::vector<int> hip(p, 0);
-    std::vector<std::thread> th;
-    th.reserve(p);
-    for (int r = 0; r < p; ++r)
-        th.emplace_back([&, r] {
-            st[r] = f(r);
-            hip[r] = t_last_hip;
-        });
-    for (auto &t : th) t.join();
-    for (int r = 0; r < p; ++r)
-        if (st[r]) {
-            t_last_hip = hip[r];
-            return st[r];
-        }
-    return LABSORT_OK;
-}
-
-int exchange_peer(const ExPlan &P, std::vector<RankState> &R) {
-    const int p = P.p;
-    for (int i = 0; i < p; ++i) {
-        MHIP(hipSetDevice(R[i].dev));
-        const uint32_t *src = static_cast<const uint32_t *>(R[i].keys.p);
-        for (int j = 0; j < p; ++j) {
-            const size_t c = P.count(i, j);
-            if (!c) continue;
-            uint32_t *dst = static_cast<uint32_t *>(R[j].recv.p) + P.roff(j, i);
-            MHIP(hipMemcpyPeerAsync(dst, R[j].dev, src + P.cut[(size_t)i * (p + 1) + j], R[i].dev, c * 4, R[i].s));
-        }
-        MHIP(hipEventRecord(R[i].ev, R[i].s));
-    }
-    for (int j = 0; j < p; ++j) {
-        MHIP(hipSetDevice(R[j].dev));
-        for (int i = 0; i < p; ++i)
-            if (i != j) MHIP(hipStreamWaitEvent(R[j].s, R[i].ev, 0));
-    }
-    return LABSORT_OK;
-}
-
-int exchange_rccl(const ExPlan &P, std::vector<RankState> &R) {
-    const int p = P.p;
-    std::vector<int> devs(p);
-    for (int r = 0; r < p; ++r) devs[r] = R[r].dev;
-    if (g_rccl.devs != devs) {
-        g_rccl.comms.assign(p, nullptr);
-        if (g_rccl.init(g_rccl.comms.data(), p, devs.data()) != ncclSuccess) return LABSORT_ERR_HIP;
-        g_rccl.devs = devs;
-    }
-    for (int i = 0; i < p && p > 1; ++i) {  // the piece a rank keeps: a local copy
-        const size_t c = P.count(i, i);
-        if (!c) continue;
-        MHIP(hipSetDevice(R[i].dev));
-        MHIP(hipMemcpyAsync(static_cast<uint32_t *>(R[i].recv.p) + P.roff(i, i),
-                            static_cast<const uint32_t *>(R[i].keys.p) + P.cut[(size_t)i * (p + 1) + i], c * 4,
-                            hipMemcpyDeviceToDevice, R[i].s));
-    }
-    if (g_rccl.gstart() != ncclSuccess) return LABSORT_ERR_HIP;
-    int bad = 0;
-    // (one rank: the send to itself goes through RCCL too -- the 1-GPU check of this path)
-    for (int i = 0; i < p && !bad; ++i) {
-        for (int j = 0; j < p && !bad; ++j) {
-            if (j == i && p > 1) continue;
-            const size_t cs = P.count(i, j), cr = P.count(j, i);
-            if (cs && g_rccl.send(static_cast<const uint32_t *>(R[i].keys.p) + P.cut[(size_t)i * (p + 1) + j], cs,
-                                  ncclUint32, j, g_rccl.comms[i], R[i].s) != ncclSuccess)
-                bad = 1;
-            if (cr && g_rccl.recv(static_cast<uint32_t *>(R[i].recv.p) + P.roff(i, j), cr, ncclUint32, j,
-                                  g_rccl.comms[i], R[i].s) != ncclSuccess)
-                bad = 1;
-        }
-    }
-    if (g_rccl.gend() != ncclSuccess || bad) return LABSORT_ERR_HIP;
-    return LABSORT_OK;
+// LABSORT_PIN=1: page-lock the caller's array for the call (hipHostRegister), so the p
+// ranks' copies run at the links' pinned rate instead of through the runtime's
+// pageable staging buffers
+bool pin_requested() {
+    const char *e = std::getenv("LABSORT_PIN");
+    return e && !std::strcmp(e, "1");
 }
 
 int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, int transport) {
@@ -312,14 +606,18 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
         if (devs[r] < 0 || devs[r] >= ndev) return LABSORT_ERR_ARG;
         for (int q = 0; q < r; ++q) distinct = distinct && devs[q] != devs[r];
     }
-    if (transport == LABSORT_XFER_AUTO) transport = (distinct && p > 1) ? LABSORT_XFER_RCCL : LABSORT_XFER_PEER;
+    // AUTO: the peer-copy transport (measured on hardware); RCCL on request
+    if (transport == LABSORT_XFER_AUTO) transport = LABSORT_XFER_PEER;
     if (transport == LABSORT_XFER_RCCL && !distinct) return LABSORT_ERR_ARG;  // RCCL: one rank per device
-    if (transport == LABSORT_XFER_RCCL && !g_rccl.load()) return LABSORT_ERR_HIP;
     if ((int)g_ranks.size() < p) g_ranks.resize(p);
-    std::vector<RankState> &R = g_ranks;
     for (int r = 0; r < p; ++r)
-        if (int st = bind_rank(R[r], devs[r])) return st;
-    if (transport == LABSORT_XFER_PEER) {
+        if (int st = bind_rank(g_ranks[r], devs[r])) return st;
+    ThreadShared sh(p);
+    sh.dev = devs;
+    if (transport == LABSORT_XFER_RCCL) {
+        if (int st = rccl_comms(devs)) return st;
+        sh.comms = g_comms;
+    } else {
         for (int a = 0; a < p; ++a)
             for (int b = 0; b < p; ++b) {
                 if (devs[a] == devs[b]) continue;
@@ -332,144 +630,82 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
                 (void)hipGetLastError();
             }
     }
-    ExPlan P;
-    P.p = p;
-    P.m.resize(p);
+    std::vector<hipEvent_t> sent_ev(p, nullptr);  // each rank's "my sends are queued" event
+    for (int r = 0; r < p; ++r) {
+        MHIP(hipSetDevice(devs[r]));
+        MHIP(hipEventCreateWithFlags(&sent_ev[r], hipEventDisableTiming));
+        sh.sent[r] = sent_ev[r];
+    }
+    const bool pin = pin_requested();
+    if (pin) MHIP(hipHostRegister(h, n * 4, hipHostRegisterDefault));
     std::vector<size_t> off(p + 1);
     for (int r = 0; r <= p; ++r) off[r] = (size_t)((unsigned __int128)n * r / p);
-    for (int r = 0; r < p; ++r) P.m[r] = off[r + 1] - off[r];
-    const size_t s = samples_per_rank(p);
-    std::vector<std::vector<uint32_t>> samples(p, std::vector<uint32_t>(s));
-    std::vector<double> t_h2d(p, 0), t_sort(p, 0);
-    for (int i = 0; i < LABSORT_MULTI_PHASES; ++i) g_phase_ms[i] = 0;
-    double t0 = now_ms();
-
-    // 1. H2D + local sort + sample, one host thread per rank
-    int st = for_ranks(p, [&](int r) -> int {
-        RankState &Q = R[r];
-        const size_t m = P.m[r];
-        MHIP(hipSetDevice(Q.dev));
-        if (!m) return LABSORT_OK;
-        if (int e = grow(Q.keys, m * 4)) return e;
-        const size_t wsb = labsort_workspace_bytes(m, LABSORT_ALGO_AUTO);
-        if (int e = grow(Q.ws, wsb)) return e;
-        if (int e = grow(Q.small, std::max(s, (size_t)4 * p) * 4)) return e;
-        const double a = now_ms();
-        MHIP(hipMemcpyAsync(Q.keys.p, h + off[r], m * 4, hipMemcpyHostToDevice, Q.s));
-        MHIP(hipStreamSynchronize(Q.s));
-        const double b = now_ms();
-        if (int e = labsort_sort_device(Q.keys.p, Q.keys.p, m, key_type, LABSORT_ALGO_AUTO, Q.ws.p, Q.ws.bytes, Q.s))
-            return e;
-        if (int e = labsort_workspace_status(Q.ws.p, m, LABSORT_ALGO_AUTO, Q.s)) return e;  // synchronises
-        t_h2d[r] = b - a;
-        t_sort[r] = now_ms() - b;
-        k_sample<<<(unsigned)((s + 255) / 256), 256, 0, Q.s>>>(static_cast<const uint32_t *>(Q.keys.p), m, (uint32_t)s,
-                                                               static_cast<uint32_t *>(Q.small.p));
-        MHIP(hipGetLastError());
-        MHIP(hipMemcpyAsync(samples[r].data(), Q.small.p, s * 4, hipMemcpyDeviceToHost, Q.s));
-        MHIP(hipStreamSynchronize(Q.s));
-        return LABSORT_OK;
-    });
-    if (st) return st;
-    double t1 = now_ms();
-    g_phase_ms[0] = *std::max_element(t_h2d.begin(), t_h2d.end());
-    g_phase_ms[1] = *std::max_element(t_sort.begin(), t_sort.end());
-
-    // 2-3. splitters and cut points
-    if (p > 1) {
-        const std::vector<Splitter> spl = choose_splitters(p, P.m, samples, flip);
-        // every rank's bound queries at once, one host thread per rank
-        const std::vector<uint32_t> vals = plan_values(spl, p, flip);
-        std::vector<std::vector<uint32_t>> bounds(p, std::vector<uint32_t>(vals.size(), 0u));
-        st = for_ranks(p, [&](int r) -> int {
-            RankState &Q = R[r];
-            if (!P.m[r]) return LABSORT_OK;
-            MHIP(hipSetDevice(Q.dev));
-            uint32_t *d = static_cast<uint32_t *>(Q.small.p);
-            MHIP(hipMemcpyAsync(d, vals.data(), vals.size() * 4, hipMemcpyHostToDevice, Q.s));
-            MHIP(launch_upper_bound(static_cast<const uint32_t *>(Q.keys.p), P.m[r], flip, d, vals.size(),
-                                    d + vals.size(), Q.s));
-            MHIP(hipMemcpyAsync(bounds[r].data(), d + vals.size(), vals.size() * 4, hipMemcpyDeviceToHost, Q.s));
-            MHIP(hipStreamSynchronize(Q.s));
-            return LABSORT_OK;
+    std::vector<int> st(p, LABSORT_OK), hip(p, 0);
+    std::vector<dist::Result> res(p);
+    std::vector<std::vector<double>> ph(p, std::vector<double>(LABSORT_MULTI_PHASES, 0.0));
+    const double t0 = now_ms();
+    std::vector<std::thread> th;
+    th.reserve(p);
+    for (int r = 0; r < p; ++r)
+        th.emplace_back([&, r] {
+            t_last_hip = 0;
+            RankState &R = g_ranks[r];
+            int e = hipSetDevice(R.dev) == hipSuccess ? LABSORT_OK : LABSORT_ERR_HIP;
+            HipRankOps ops{R, R.own, key_type, true};
+            ThreadComm comm{sh, r, R.own, transport == LABSORT_XFER_RCCL};
+            if (!e) e = dist::sort_rank(ops, comm, h + off[r], off[r + 1] - off[r], flip, h, res[r]);
+            const int f = ops.finish();  // drain the streams even after a failure
+            if (!e) e = f;
+            if (e) sh.abort();
+            else ops.phases(ph[r].data(), true);
+            st[r] = e;
+            hip[r] = t_last_hip;
         });
-        if (st) return st;
-        st = make_plan(P, spl, flip, [&](int r, const std::vector<uint32_t> &, std::vector<uint32_t> &out) -> int {
-            out = bounds[r];
-            return LABSORT_OK;
-        });
-        if (st) return st;
-    } else {
-        make_plan(P, {}, flip, nullptr);
+    for (auto &t : th) t.join();
+    const double t1 = now_ms();
+    for (int r = 0; r < p; ++r) {
+        (void)hipSetDevice(devs[r]);
+        (void)hipEventDestroy(sent_ev[r]);
     }
-    for (int j = 0; j < p; ++j)
-        if (P.total(j) > 0x7FFFFFFFu) return LABSORT_ERR_ARG;  // one rank's range beyond a device merge
-    double t2 = now_ms();
-    g_phase_ms[2] = t2 - t1;
-
-    // 4. exchange into the receive buffers
-    {  // the most key bytes one rank sends to its peers (the xGMI volume per link set)
-        size_t worst = 0;
-        for (int i = 0; i < p; ++i) {
-            size_t b = 0;
-            for (int j = 0; j < p; ++j)
-                if (j != i) b += P.count(i, j) * 4;
-            worst = std::max(worst, b);
-        }
-        g_sent_bytes = worst;
+    if (pin) MHIP(hipHostUnregister(h));
+    // the first rank that failed for a reason of its own (others report the abort)
+    for (int pass = 0; pass < 2; ++pass)
+        for (int r = 0; r < p; ++r)
+            if (st[r] && (pass == 1 || st[r] != LABSORT_ERR_DEVICE || hip[r])) {
+                t_last_hip = hip[r];
+                return st[r];
+            }
+    for (int i = 0; i < LABSORT_MULTI_PHASES; ++i) g_phase_ms[i] = 0.0;
+    size_t sent = 0;
+    for (int r = 0; r < p; ++r) {
+        for (int i = 0; i < 6; ++i) g_phase_ms[i] = std::max(g_phase_ms[i], ph[r][i]);
+        sent = std::max(sent, (size_t)res[r].sent);
     }
-    for (int j = 0; j < p; ++j) {
-        MHIP(hipSetDevice(R[j].dev));
-        if (int e = grow(R[j].recv, P.total(j) * 4)) return e;
-        if (int e = grow(R[j].out, P.total(j) * 4)) return e;
-        if (int e = grow(R[j].kmws, labsort_merge_runs_workspace_bytes(P.total(j)))) return e;
-    }
-    const bool direct = p == 1 && transport != LABSORT_XFER_RCCL;  // one rank: nothing to exchange
-    st = direct ? LABSORT_OK : transport == LABSORT_XFER_RCCL ? exchange_rccl(P, R) : exchange_peer(P, R);
-    if (st) return st;
-    for (int j = 0; j < p; ++j) {
-        MHIP(hipSetDevice(R[j].dev));
-        MHIP(hipStreamSynchronize(R[j].s));
-    }
-    double t3 = now_ms();
-    g_phase_ms[3] = t3 - t2;
-
-    // 5. K-way merge of the received runs, D2H of each range to its global offset
-    std::vector<size_t> goff(p + 1, 0);
-    for (int j = 0; j < p; ++j) goff[j + 1] = goff[j] + P.total(j);
-    std::vector<double> t_merge(p, 0), t_d2h(p, 0);
-    st = for_ranks(p, [&](int j) -> int {
-        RankState &Q = R[j];
-        const size_t tot = P.total(j);
-        MHIP(hipSetDevice(Q.dev));
-        if (!tot) return LABSORT_OK;
-        const double a = now_ms();
-        const uint32_t *res;
-        if (direct) {
-            res = static_cast<const uint32_t *>(Q.keys.p);
-        } else {
-            std::vector<size_t> o(P.recv_off.begin() + (size_t)j * (p + 1), P.recv_off.begin() + (size_t)(j + 1) * (p + 1));
-            if (int e = labsort_merge_runs(Q.recv.p, Q.out.p, o.data(), p, key_type, Q.kmws.p, Q.kmws.bytes, Q.s))
-                return e;
-            res = static_cast<const uint32_t *>(Q.out.p);
-        }
-        MHIP(hipStreamSynchronize(Q.s));
-        const double b = now_ms();
-        MHIP(hipMemcpyAsync(h + goff[j], res, tot * 4, hipMemcpyDeviceToHost, Q.s));
-        MHIP(hipStreamSynchronize(Q.s));
-        t_merge[j] = b - a;
-        t_d2h[j] = now_ms() - b;
-        return LABSORT_OK;
-    });
-    if (st) return st;
-    g_phase_ms[4] = *std::max_element(t_merge.begin(), t_merge.end());
-    g_phase_ms[5] = *std::max_element(t_d2h.begin(), t_d2h.end());
-    g_phase_ms[6] = now_ms() - t0;
+    g_phase_ms[6] = t1 - t0;
+    g_sent_bytes = sent;
+    g_range_counts.assign(p, 0);
+    for (int r = 0; r < p; ++r) g_range_counts[r] = (size_t)res[r].count;
     return LABSORT_OK;
 }
 
 }  // namespace
 }  // namespace labsort
+
+// ---------------------------------------------------------------------------------
+// one process per GPU: the communicator handle of the C-ABI
+// ---------------------------------------------------------------------------------
+struct labsort_comm {
+    int kind = 0;  // 1 RCCL, 2 host callbacks
+    int p = 0, me = 0, dev = -1;
+    ncclComm_t nc = nullptr;
+    labsort_host_coll cb{};
+    labsort::RankState R;
+    labsort::Buf stage;
+    std::vector<uint32_t> hs, hr;
+    double phase[LABSORT_MULTI_PHASES] = {};
+    size_t sent = 0;
+    int last_hip = 0;
+};
 
 using namespace labsort;
 
@@ -486,6 +722,7 @@ int labsort_sort_host_ranks(void *h_keys, size_t n, int key_type, int nranks, co
     std::lock_guard<std::mutex> lk(g_mu);
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess) cur = 0;
+    t_last_hip = 0;
     const int st = sort_ranks(static_cast<uint32_t *>(h_keys), n, key_type, nranks, devices, transport);
     const int hip = t_last_hip;
     (void)hipSetDevice(cur);
@@ -499,6 +736,13 @@ int labsort_sort_host_multi(void *h_keys, size_t n, int key_type, int ngpus) {
 
 int labsort_multi_last_hip_error(void) { return t_last_hip; }
 
+const char *labsort_multi_error_detail(void) {
+    static thread_local std::string copy;
+    std::lock_guard<std::mutex> lk(g_err_mu);
+    copy = g_detail;
+    return copy.c_str();
+}
+
 int labsort_multi_timing(double *phase_ms, int nphases, size_t *max_sent_bytes) {
     if (!phase_ms || nphases < 0 || nphases > LABSORT_MULTI_PHASES) return LABSORT_ERR_ARG;
     std::lock_guard<std::mutex> lk(g_mu);
@@ -507,40 +751,155 @@ int labsort_multi_timing(double *phase_ms, int nphases, size_t *max_sent_bytes) 
     return LABSORT_OK;
 }
 
+int labsort_multi_range_counts(size_t *counts, int nranks) {
+    if (!counts || nranks < 0) return LABSORT_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((size_t)nranks > g_range_counts.size()) return LABSORT_ERR_ARG;
+    for (int r = 0; r < nranks; ++r) counts[r] = g_range_counts[r];
+    return LABSORT_OK;
+}
+
 int labsort_multi_plan(const uint32_t *const *h_shards, const size_t *m, int nranks, int key_type,
                        size_t *h_cuts) {
     if (nranks < 1 || nranks > LABSORT_MULTI_MAX_RANKS || !h_shards || !m || !h_cuts) return LABSORT_ERR_ARG;
     const uint32_t flip = key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u;
     const int p = nranks;
-    ExPlan P;
-    P.p = p;
-    P.m.assign(m, m + p);
-    const size_t s = samples_per_rank(p);
-    std::vector<std::vector<uint32_t>> samples(p, std::vector<uint32_t>(s));
-    size_t total = 0;
+    const size_t s = dist::samples_per_rank(p);
+    std::vector<uint64_t> ms(m, m + p);
+    std::vector<uint32_t> samples((size_t)p * s, 0u);
     for (int r = 0; r < p; ++r) {
-        total += m[r];
         if (m[r] && !h_shards[r]) return LABSORT_ERR_ARG;
-        for (size_t k = 0; m[r] && k < s; ++k) samples[r][k] = h_shards[r][sample_pos(m[r], s, k)];
+        for (size_t k = 0; m[r] && k < s; ++k) samples[(size_t)r * s + k] = h_shards[r][dist::sample_pos(m[r], s, k)];
     }
-    int st = LABSORT_OK;
-    if (p > 1 && total) {
-        const std::vector<Splitter> spl = choose_splitters(p, P.m, samples, flip);
-        st = make_plan(P, spl, flip, [&](int r, const std::vector<uint32_t> &vals, std::vector<uint32_t> &out) -> int {
-            const uint32_t *a = h_shards[r];
-            for (size_t v = 0; v < vals.size(); ++v)
-                out[v] = (uint32_t)(std::upper_bound(a, a + m[r], vals[v] ^ flip,
-                                                     [flip](uint32_t x, uint32_t y) { return x < (y ^ flip); }) -
-                                    a);
-            return LABSORT_OK;
-        });
-    } else {  // one rank, or no keys: every rank keeps its (empty) shard as its last piece
-        P.cut.assign((size_t)p * (p + 1), 0);
-        for (int r = 0; r < p; ++r) P.cut[(size_t)r * (p + 1) + p] = m[r];
+    const std::vector<dist::Splitter> spl = dist::choose_splitters(p, ms.data(), samples.data(), s, flip);
+    const std::vector<uint32_t> vals = dist::plan_values(spl, p, flip);
+    std::vector<uint64_t> cut(p + 1);
+    for (int r = 0; r < p; ++r) {
+        const uint32_t *a = h_shards[r];
+        std::vector<uint32_t> ub(vals.size());
+        for (size_t v = 0; v < vals.size(); ++v)  // number of keys <= vals[v] in key order
+            ub[v] = (uint32_t)(std::upper_bound(a, a + m[r], vals[v] ^ flip,
+                                                [flip](uint32_t x, uint32_t y) { return x < (y ^ flip); }) -
+                               a);
+        if (int st = dist::rank_cuts(r, m[r], spl, ub.data(), p, cut.data())) return st;
+        for (int j = 0; j <= p; ++j) h_cuts[(size_t)r * (p + 1) + j] = (size_t)cut[j];
     }
-    if (st) return st;
-    std::copy(P.cut.begin(), P.cut.end(), h_cuts);
     return LABSORT_OK;
 }
+
+int labsort_comm_unique_id(void *id) {
+    if (!id) return LABSORT_ERR_ARG;
+    if (!g_rccl.load()) return LABSORT_ERR_HIP;
+    ncclUniqueId u;
+    NCHK("ncclGetUniqueId", g_rccl.uid(&u));
+    memcpy(id, &u, sizeof u);
+    return LABSORT_OK;
+}
+
+int labsort_comm_init_rccl(labsort_comm_t *comm, const void *id, int nranks, int rank) {
+    if (!comm || !id || nranks < 1 || rank < 0 || rank >= nranks) return LABSORT_ERR_ARG;
+    *comm = nullptr;
+    if (!g_rccl.load()) return LABSORT_ERR_HIP;
+    labsort_comm *c = new labsort_comm;
+    c->kind = 1;
+    c->p = nranks;
+    c->me = rank;
+    if (hipGetDevice(&c->dev) != hipSuccess) {
+        delete c;
+        return LABSORT_ERR_HIP;
+    }
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    const ncclResult_t r = g_rccl.init_rank(&c->nc, nranks, u, rank);
+    if (r != ncclSuccess) {
+        delete c;
+        return g_rccl.fail("ncclCommInitRank", r);
+    }
+    *comm = c;
+    return LABSORT_OK;
+}
+
+int labsort_comm_init_host(labsort_comm_t *comm, int nranks, int rank, const labsort_host_coll *coll) {
+    if (!comm || !coll || !coll->allgather || !coll->alltoallv || nranks < 1 || rank < 0 || rank >= nranks)
+        return LABSORT_ERR_ARG;
+    labsort_comm *c = new labsort_comm;
+    c->kind = 2;
+    c->p = nranks;
+    c->me = rank;
+    c->cb = *coll;
+    if (hipGetDevice(&c->dev) != hipSuccess) {
+        delete c;
+        return LABSORT_ERR_HIP;
+    }
+    *comm = c;
+    return LABSORT_OK;
+}
+
+int labsort_comm_destroy(labsort_comm_t c) {
+    if (!c) return LABSORT_OK;
+    int st = LABSORT_OK;
+    if (c->nc) {
+        const ncclResult_t r = g_rccl.destroy(c->nc);
+        if (r != ncclSuccess) st = g_rccl.fail("ncclCommDestroy", r);
+    }
+    if (c->R.dev >= 0) {
+        (void)hipSetDevice(c->R.dev);
+        for (Buf *b : {&c->R.x, &c->R.y, &c->R.ws, &c->R.mws, &c->R.recv, &c->R.out, &c->R.small, &c->R.part,
+                       &c->R.errs, &c->stage})
+            if (b->p) (void)hipFree(b->p);
+        for (hipStream_t s : {c->R.own, c->R.copy})
+            if (s) (void)hipStreamDestroy(s);
+        for (hipEvent_t e : c->R.chunk_ev) (void)hipEventDestroy(e);
+        for (hipEvent_t e : c->R.range_ev) (void)hipEventDestroy(e);
+        for (hipEvent_t e : c->R.tev) (void)hipEventDestroy(e);
+    }
+    delete c;
+    return st;
+}
+
+int labsort_dist_sort(labsort_comm_t c, const void *d_keys, size_t m, int key_type, void *stream,
+                      const void **d_result, size_t *count, size_t *global_offset) {
+    if (!c || !d_result || !count || (m && !d_keys)) return LABSORT_ERR_ARG;
+    if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
+    if (m > labsort_max_keys(LABSORT_ALGO_RADIX)) return LABSORT_ERR_ARG;
+    t_last_hip = 0;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || cur != c->dev) return LABSORT_ERR_ARG;  // the comm's device
+    if (int st = bind_rank(c->R, c->dev)) return st;
+    hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the null stream, as everywhere in the C-ABI
+    HipRankOps ops{c->R, s, key_type, false};
+    dist::Result res;
+    const double t0 = now_ms();
+    int st;
+    if (c->kind == 1) {
+        RcclComm comm{c->nc, c->p, c->me, s, c->stage};
+        st = dist::sort_rank(ops, comm, static_cast<const uint32_t *>(d_keys), m,
+                             key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u, nullptr, res);
+    } else {
+        HostCbComm comm{c->cb, c->p, c->me, s, c->hs, c->hr};
+        st = dist::sort_rank(ops, comm, static_cast<const uint32_t *>(d_keys), m,
+                             key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u, nullptr, res);
+    }
+    const int f = ops.finish();
+    if (!st) st = f;
+    c->last_hip = t_last_hip;
+    if (st) return st;
+    ops.phases(c->phase, false);
+    c->phase[6] = now_ms() - t0;
+    c->sent = res.sent;
+    *d_result = res.data;
+    *count = res.count;
+    if (global_offset) *global_offset = res.goff;
+    return LABSORT_OK;
+}
+
+int labsort_dist_timing(labsort_comm_t c, double *phase_ms, int nphases, size_t *sent_bytes) {
+    if (!c || !phase_ms || nphases < 0 || nphases > LABSORT_MULTI_PHASES) return LABSORT_ERR_ARG;
+    for (int i = 0; i < nphases; ++i) phase_ms[i] = c->phase[i];
+    if (sent_bytes) *sent_bytes = c->sent;
+    return LABSORT_OK;
+}
+
+int labsort_dist_last_hip_error(labsort_comm_t c) { return c ? c->last_hip : 0; }
 
 }  // extern "C"

@@ -15,20 +15,19 @@ steps for p ranks.  `partial=True` moves only the keys that cross: both sides
 first swap a strided sample of their shards, bracket the split point, swap the
 bracketing window, agree on the exact split k, then send k keys each way.
 
-`dist_sort_splitters` is the all-link form (the default of bench.py): every rank
-sorts its shard, the ranks agree on p-1 splitters from a regular sample of every
-shard (one all_gather), cut their sorted shards at the splitters
-(`labsort_upper_bound`), send piece j to rank j with pairwise send/recv posted to
-all peers at once (so all 7 xGMI links of a node carry data together instead of
-one per step) straight into one buffer, and merge the p received runs in rank
-order in one K-way `labsort_merge_runs` pass (or a tree of `labsort_merge` passes;
-A before B on ties).  Rank r then holds the r-th contiguous
-range of the sorted array; range sizes follow the splitters (within a few percent
-of n/p on varied data; skewed data with a heavy repeated key can unbalance them).
+`dist_sort_splitters` is the all-link form (the default of bench.py) and a thin
+caller of the product: labsort_dist_sort runs the schedule of csrc/dist_plan.h in C++
+(the same code the one-process multi-GPU path and the oracle's CPU instantiation run):
+every rank sorts its shard, the ranks agree on p-1 (key, rank, position) splitters
+from a regular sample of every shard, cut their sorted shards at them, send piece j to
+rank j with pairwise send/recv posted to all peers at once (all 7 xGMI links of a GPU
+carry data together instead of one per step), and merge the p received runs in rank
+order.  Communicators: RCCL (make_comm(backend="nccl"): ncclCommInitRank with rank 0's
+unique id) or host-staged gloo collectives (GlooColl, tests).
 
-Local operations are pluggable (`Ops`): the product uses liblabsort.so on the
-rank's GPU (`HipOps`); the CPU tests inject an oracle-backed implementation so the
-exchange schedule is exercised with the gloo backend on machines without GPUs.
+For the bitonic network the local operations are pluggable (`Ops`): liblabsort.so on
+the rank's GPU (`HipOps`), or numpy in the CPU tests, so that schedule is exercised
+with the gloo backend on machines without GPUs.
 Communication is pluggable too (`P2PComm` = torch.distributed; `HostStagedComm`
 stages device tensors through host memory for a CPU backend in tests).
 """
@@ -53,34 +52,7 @@ class Ops:
         """elements d0..d1-1 of merge(a, b), a before b on ties"""
         raise NotImplementedError
 
-    def merge_runs(self, buf: torch.Tensor, offsets: list) -> torch.Tensor:
-        """Merge of the sorted runs buf[offsets[q]:offsets[q+1]] in run order (equal
-        keys keep run order).  Default: a tree of pairwise merges."""
-        runs = [buf[offsets[q]:offsets[q + 1]] for q in range(len(offsets) - 1)]
-        while len(runs) > 1:
-            nxt = []
-            for i in range(0, len(runs) - 1, 2):
-                x, y = runs[i], runs[i + 1]
-                if x.numel() == 0:
-                    nxt.append(y)
-                elif y.numel() == 0:
-                    nxt.append(x)
-                else:
-                    nxt.append(self.merge(x, y, 0, x.numel() + y.numel()))
-            if len(runs) % 2:
-                nxt.append(runs[-1])
-            runs = nxt
-        return runs[0].contiguous() if runs else buf[:0]
-
     def key_le(self, x: int, y: int) -> bool:
-        raise NotImplementedError
-
-    def argsort(self, t: torch.Tensor) -> torch.Tensor:
-        """Stable argsort of int32-stored keys in key order (int64 indices)."""
-        return torch.argsort(self.order(t), stable=True)
-
-    def upper_bound(self, a: torch.Tensor, values: torch.Tensor) -> torch.Tensor:
-        """int64 tensor: number of keys of sorted `a` <= each value (key order)"""
         raise NotImplementedError
 
     def order(self, t: torch.Tensor) -> torch.Tensor:
@@ -90,15 +62,10 @@ class Ops:
 
 
 class HipOps(Ops):
-    """liblabsort.so on the current GPU."""
+    """liblabsort.so on the current GPU (local operations of the bitonic network)."""
 
-    def __init__(self, ls, key: str = "u32", local_algo: str = "radix", stream=None, kway: bool = True):
+    def __init__(self, ls, key: str = "u32", local_algo: str = "radix", stream=None):
         self.ls, self.key, self.algo, self.stream = ls, key, local_algo, stream
-        # kway: merge the received runs with labsort_merge_runs (pair passes over explicit
-        # runs in C++) instead of a Python tree of labsort_merge calls.  Measured on
-        # MI355X for 2^28 keys in p runs (profiles/r17_dist_merge_step.jsonl): p = 2 / 4 /
-        # 8: 0.53 / 1.04 / 1.66 ms, tree 0.75 / 1.45 / 2.22 ms
-        self.kway = kway
         self._ws = None
         self._part = None
 
@@ -116,19 +83,6 @@ class HipOps(Ops):
         self.ls.workspace_status(ws, t.numel(), self.algo, stream=self.stream)
         return out
 
-    def argsort(self, t):
-        """Stable argsort by the labsort key/value sort of (key, index) pairs."""
-        n = t.numel()
-        if n == 0:
-            return torch.zeros(0, dtype=torch.int64, device=t.device)
-        idx = torch.arange(n, dtype=torch.int32, device=t.device)
-        ko, vo = torch.empty_like(t), torch.empty_like(idx)
-        ws = torch.empty(max(self.ls.pairs_workspace_bytes(n, "auto"), 256), dtype=torch.uint8, device=t.device)
-        self.ls.sort_pairs_device(t.contiguous(), idx, ko, vo, n, key=self.key, algo="auto", workspace=ws,
-                                  stream=self.stream)
-        self.ls.pairs_workspace_status(ws, n, "auto", stream=self.stream)
-        return vo.to(torch.int64)
-
     def merge(self, a, b, d0, d1):
         out = torch.empty(max(d1 - d0, 1), dtype=torch.int32, device=a.device if a.numel() else b.device)
         parts = self.ls.merge_parts(d1 - d0)
@@ -137,34 +91,9 @@ class HipOps(Ops):
         self.ls.merge(a, a.numel(), b, b.numel(), out, d0, d1, self._part, key=self.key, stream=self.stream)
         return out[: d1 - d0]
 
-    def merge_runs(self, buf, offsets):
-        """One K-way pass (labsort_merge_runs, K <= 8) when self.kway (the default);
-        otherwise, and for more than 8 runs, the merge tree."""
-        if not self.kway or len(offsets) - 1 > 8:
-            return super().merge_runs(buf, offsets)
-        n = offsets[-1] - offsets[0]
-        out = torch.empty(max(n, 1), dtype=torch.int32, device=buf.device)
-        if n:
-            o = [x - offsets[0] for x in offsets]
-            self.ls.merge_runs(buf[offsets[0]:offsets[-1]], out, o, key=self.key, workspace=self._kmws(n),
-                               stream=self.stream)
-        return out[:n]
-
-    def _kmws(self, n):
-        need = max(self.ls.merge_runs_workspace_bytes(n), 256)
-        if getattr(self, "_km", None) is None or self._km.numel() < need:
-            self._km = torch.empty(need, dtype=torch.uint8, device="cuda")
-        return self._km
-
     def key_le(self, x, y):
         f = 0x80000000 if self.key == "i32" else 0
         return ((x & 0xFFFFFFFF) ^ f) <= ((y & 0xFFFFFFFF) ^ f)
-
-    def upper_bound(self, a, values):
-        out = torch.empty(values.numel(), dtype=torch.int32, device=a.device)
-        self.ls.upper_bound(a, a.numel(), values.contiguous(), values.numel(), out, key=self.key,
-                            stream=self.stream)
-        return out.to(torch.int64)
 
 
 class P2PComm:
@@ -194,33 +123,6 @@ class P2PComm:
         self._sync()
         self.exchange_s += time.perf_counter() - t0
 
-    def exchange_all(self, sends: list, recvs: list, rank: int) -> None:
-        """sends[j] -> rank j, recvs[j] <- rank j for every peer j != rank, all posted
-        together (one group: every xGMI link busy at once); empty pieces are skipped."""
-        self.sent_bytes += sum(x.numel() * x.element_size() for j, x in enumerate(sends) if j != rank)
-        self.p2p_rounds += 1
-        g = self.group
-        ops = []
-        for j in range(len(sends)):
-            if j == rank:
-                continue
-            if sends[j].numel():
-                ops.append(dist.P2POp(dist.isend, sends[j], j, group=g))
-            if recvs[j].numel():
-                ops.append(dist.P2POp(dist.irecv, recvs[j], j, group=g))
-        self._sync()
-        t0 = time.perf_counter()
-        if ops:
-            for r in dist.batch_isend_irecv(ops):
-                r.wait()
-        self._sync()
-        self.exchange_s += time.perf_counter() - t0
-
-    def all_gather(self, t: torch.Tensor) -> list:
-        out = [torch.empty_like(t) for _ in range(dist.get_world_size(self.group))]
-        dist.all_gather(out, t, group=self.group)
-        return out
-
 
 class HostStagedComm(P2PComm):
     """Test adapter: device tensors are staged through host memory and exchanged
@@ -232,17 +134,6 @@ class HostStagedComm(P2PComm):
         hr = torch.empty_like(hs)
         super().exchange(hs, hr, partner)
         recv.copy_(hr)
-
-    def exchange_all(self, sends, recvs, rank):
-        hs = [x.cpu() if j != rank else x[:0].cpu() for j, x in enumerate(sends)]
-        hr = [torch.empty(x.shape, dtype=x.dtype) if j != rank else x[:0].cpu() for j, x in enumerate(recvs)]
-        super().exchange_all(hs, hr, rank)
-        for j, (d, h) in enumerate(zip(recvs, hr)):
-            if j != rank and h.numel():
-                d.copy_(h)
-
-    def all_gather(self, t):
-        return [x.to(t.device) for x in super().all_gather(t.cpu())]
 
 
 def schedule(world: int):
@@ -303,9 +194,14 @@ def _first_false(p: torch.Tensor) -> int:
 
 def _on_stream(ops):
     """Run the schedule's torch work on the stream the local operations use, so a
-    caller that passes HipOps(stream=s) without entering it gets ordered work."""
+    caller that passes HipOps(stream=s) without entering it gets ordered work (a raw
+    hipStream_t handle is wrapped as an external stream)."""
     s = getattr(ops, "stream", None)
-    return torch.cuda.stream(s) if s is not None else contextlib.nullcontext()
+    if s is None:
+        return contextlib.nullcontext()
+    if isinstance(s, int):
+        s = torch.cuda.ExternalStream(s)
+    return torch.cuda.stream(s)
 
 
 def dist_sort(local: torch.Tensor, ops: Ops, group=None, partial: bool = True, stride: int = 4096,
@@ -349,69 +245,55 @@ def _dist_sort(local, ops, group, partial, stride, copy_input, comm):
     return a
 
 
-def dist_sort_splitters(local: torch.Tensor, ops: Ops, group=None, comm=None, copy_input: bool = False,
-                        oversample: int = 1024) -> torch.Tensor:
-    """Sort the global array whose rank-r shard is `local` with one all-peer exchange.
-    Returns this rank's contiguous range of the sorted array (ranges in rank order).
+class GlooColl:
+    """Host collectives over a torch.distributed group (gloo): the labsort_host_coll
+    callbacks of a host-staged labsort communicator (DistComm.host).  The CPU tests use
+    it with the oracle's host instantiation of the schedule, the GPU tests to run several
+    ranks of the HIP schedule on one GPU."""
 
-    Splitters are (key, source rank, position) triples, so runs of one repeated key
-    are cut between ranks like any other keys: every range stays within the sample
-    granularity (about n/oversample keys) of its share, even for constant input."""
-    with _on_stream(ops):
-        return _dist_sort_splitters(local, ops, group, comm, copy_input, oversample)
+    def __init__(self, group=None):
+        self.group = group
+        self.world = dist.get_world_size(group)
+
+    def allgather(self, h_in: int, h_out: int, nbytes: int) -> None:
+        import ctypes
+        t = torch.empty(nbytes, dtype=torch.uint8)
+        ctypes.memmove(t.data_ptr(), h_in, nbytes)
+        outs = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(self.world)]
+        dist.all_gather(outs, t, group=self.group)
+        for i, o in enumerate(outs):
+            ctypes.memmove(h_out + i * nbytes, o.data_ptr(), nbytes)
+
+    def alltoallv(self, h_send: int, send_bytes: list, h_recv: int, recv_bytes: list) -> None:
+        import ctypes
+        ts, tr = sum(send_bytes), sum(recv_bytes)
+        inp = torch.empty(ts // 4, dtype=torch.int32)
+        if ts:
+            ctypes.memmove(inp.data_ptr(), h_send, ts)
+        out = torch.empty(tr // 4, dtype=torch.int32)
+        dist.all_to_all_single(out, inp, [b // 4 for b in recv_bytes], [b // 4 for b in send_bytes],
+                               group=self.group)
+        if tr:
+            ctypes.memmove(h_recv, out.data_ptr(), tr)
 
 
-def _dist_sort_splitters(local, ops, group, comm, copy_input, oversample):
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    comm = comm if comm is not None else P2PComm(group)
-    a = ops.local_sort(local, out_of_place=copy_input)
-    if world == 1:
-        return a
-    m = a.numel()
-    # regular sample of every sorted shard: (key, position); the same sample size on
-    # every rank (all_gather), positions repeat if m < s
-    s = oversample * world
-    idx = (torch.arange(s, device=a.device, dtype=torch.int64) * m) // s
-    samp = a[idx].contiguous() if m else torch.zeros(s, dtype=a.dtype, device=a.device)
-    meta = torch.cat([idx, torch.tensor([1 if m else 0], dtype=torch.int64, device=a.device)])
-    samples = comm.all_gather(samp)
-    metas = comm.all_gather(meta)
-    valid = [int(x) for x in torch.stack([mt[-1] for mt in metas]).cpu().tolist()]  # empty shards sample nothing
-    ranks_ok = [r for r in range(world) if valid[r]]
-    if not ranks_ok:
-        ranks_ok = [rank]
-    pool = torch.cat([samples[r] for r in ranks_ok])
-    pool_rank = torch.cat([torch.full((s,), r, dtype=torch.int64, device=a.device) for r in ranks_ok])
-    pool_pos = torch.cat([metas[r][:-1] for r in ranks_ok])
-    # rank order + ascending positions per rank + a stable sort by key = (key, rank, pos) order
-    srt = ops.argsort(pool)
-    q = srt[(torch.arange(1, world, device=a.device, dtype=torch.int64) * pool.numel()) // world]
-    spl_key, spl_rank, spl_pos = pool[q].contiguous(), pool_rank[q], pool_pos[q]
-    # cut j on this rank: keys before splitter j in (key, rank, pos) order
-    if m:
-        f = 0x80000000 if getattr(ops, "key", "u32") == "i32" else 0
-        o = ops.order(spl_key)
-        prev = ((o - 1).clamp(min=0) ^ f) & 0xFFFFFFFF            # key just below, in key order
-        prev = torch.where(prev >= 2**31, prev - 2**32, prev).to(torch.int32)
-        both = ops.upper_bound(a, torch.cat([spl_key, prev]))
-        ub, lb = both[:world - 1], torch.where(o == 0, torch.zeros_like(o), both[world - 1:])
-        cuts = torch.where(spl_rank > rank, ub, torch.where(spl_rank < rank, lb, spl_pos + 1))
-    else:
-        cuts = torch.zeros(world - 1, dtype=torch.int64, device=a.device)
-    bounds = [0] + [int(c) for c in cuts.cpu().tolist()] + [m]
-    sizes = torch.tensor([bounds[j + 1] - bounds[j] for j in range(world)], dtype=torch.int64, device=a.device)
-    all_sizes = torch.stack(comm.all_gather(sizes)).cpu()  # all_sizes[i][j] = rank i -> rank j
-    sends = [a[bounds[j]:bounds[j + 1]] for j in range(world)]
-    # receive every piece straight into its slot of one buffer (rank order), then merge
-    # the p runs (A before B on ties, so equal keys keep rank order)
-    counts = [int(all_sizes[i][rank]) for i in range(world)]
-    offs = [0]
-    for c in counts:
-        offs.append(offs[-1] + c)
-    buf = torch.empty(max(offs[-1], 1), dtype=a.dtype, device=a.device)
-    recvs = [buf[offs[i]:offs[i + 1]] for i in range(world)]
-    if counts[rank]:
-        recvs[rank].copy_(sends[rank])
-    comm.exchange_all([x.contiguous() for x in sends], recvs, rank)
-    return ops.merge_runs(buf, offs)
+def make_comm(ls, backend: str = "nccl", group=None):
+    """This rank's labsort communicator: RCCL (backend "nccl": rank 0's ncclUniqueId
+    broadcast over the torch.distributed group) or host-staged gloo collectives."""
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if backend != "nccl":
+        return ls.DistComm.host(world, rank, GlooColl(group))
+    uid = ls.DistComm.unique_id() if rank == 0 else bytes(128)
+    obj = [uid]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return ls.DistComm.rccl(world, rank, obj[0])
+
+
+def dist_sort_splitters(local: torch.Tensor, comm, key: str = "u32", stream=None):
+    """Sort the global array whose rank-r shard is `local` (device tensor, left
+    untouched) with the product's splitter exchange: labsort_dist_sort, the C++ schedule
+    of csrc/dist_plan.h (local radix sort, (key, rank, position) splitters from a regular
+    sample, pairwise send/recv with every peer at once, merge of the received runs in
+    rank order).  Returns (this rank's contiguous range of the sorted array as a tensor
+    viewing the communicator's buffer, its global offset)."""
+    return comm.sort_tensor(local, local.numel(), key=key, stream=stream)

@@ -1,9 +1,15 @@
-"""Multi-rank tests of the merge-split exchange (dist.py) on CPU with the gloo
-backend.  The local operations are injected (`NumpyOps`: numpy sort and a
-stable two-run merge, A before B on ties, as lab.cu:163-170) so the schedule,
-the split-count protocol and the send/recv pairing are exercised without GPUs;
-on the GPU box the same schedule runs with HipOps (liblabsort) over RCCL.
-The result is compared with the oracle's std::sort of the whole array."""
+"""Multi-rank tests of the multi-GPU merge-sort schedules on CPU with the gloo backend.
+
+* The product's splitter exchange (csrc/dist_plan.h, dist::sort_rank -- the one copy of
+  the schedule that labsort_dist_sort and labsort_sort_host_ranks run on the GPUs) is run
+  here by the oracle's host instantiation (oracle/dist_host.cpp: std::sort, std::upper_bound,
+  std::merge as rank operations) over the package's gloo host collectives (dist.GlooColl),
+  2, 4 and 8 ranks, ragged and empty shards included.
+* The bitonic merge-split network (dist.dist_sort, Python) runs with injected numpy
+  local operations (`NumpyOps`: numpy sort and a stable two-run merge, A before B on
+  ties, as lab.cu:163-170).
+Results are compared with the oracle's std::sort of the whole array.
+"""
 import importlib
 import os
 import socket
@@ -27,7 +33,51 @@ def free_port():
     return p
 
 
-def _worker(rank, world, port, cfg, q):
+def _run_cfg(O, D, rank, world, cfg):
+    m, dist_name, seed, key = cfg["m"], cfg["dist"], cfg["seed"], cfg["key"]
+    if cfg.get("exchange") == "splitters":
+        sizes = cfg.get("sizes") or [m] * world
+        first = sum(sizes[:rank])
+        shard = O.gen(sizes[rank], seed, dist_name, first=first)
+        out, goff = O.dist_sort(shard, key, world, rank, D.GlooColl(), cap=sum(sizes) + 1)
+        return out.view(np.int32).copy(), goff
+
+    class NumpyOps(D.Ops):
+        def __init__(self, key):
+            self.key = key
+            self.f = np.uint32(0x80000000 if key == "i32" else 0)
+
+        def _u(self, t):
+            return t.numpy().view(np.uint32) ^ self.f
+
+        def local_sort(self, t, out_of_place=False):
+            s = torch.from_numpy(((np.sort(self._u(t)) ^ self.f).view(np.int32)).copy())
+            if out_of_place:
+                return s
+            t.copy_(s)
+            return t
+
+        def merge(self, a, b, d0, d1):
+            cat = np.concatenate([self._u(a), self._u(b)])
+            idx = np.argsort(cat, kind="stable")  # a's elements first on ties
+            return torch.from_numpy(((cat[idx][d0:d1] ^ self.f).view(np.int32)).copy())
+
+        def key_le(self, x, y):
+            f = int(self.f)
+            return ((x & 0xFFFFFFFF) ^ f) <= ((y & 0xFFFFFFFF) ^ f)
+
+    shard = O.gen(m, seed, dist_name, first=rank * m)
+    t = torch.from_numpy(shard.view(np.int32).copy())
+    out = D.dist_sort(t, NumpyOps(key), partial=cfg["partial"], stride=cfg["stride"],
+                      copy_input=cfg.get("copy", False))
+    if cfg.get("copy", False):
+        assert torch.equal(t, torch.from_numpy(shard.view(np.int32)))  # input untouched
+    return out.numpy().copy(), None
+
+
+def _worker(rank, world, port, cfgs, q):
+    """one rank: every config in turn over one gloo group (one process spawn per rank
+    and world size keeps the CPU suite short)"""
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -35,67 +85,41 @@ def _worker(rank, world, port, cfg, q):
     try:
         import oracle as O
         D = importlib.import_module(PKG_NAME + ".dist")
-
-        class NumpyOps(D.Ops):
-            def __init__(self, key):
-                self.key = key
-                self.f = np.uint32(0x80000000 if key == "i32" else 0)
-
-            def upper_bound(self, a, values):
-                av = self._u(a)
-                vv = self._u(values)
-                return torch.from_numpy(np.searchsorted(av, vv, side="right").astype(np.int64))
-
-            def _u(self, t):
-                return t.numpy().view(np.uint32) ^ self.f
-
-            def local_sort(self, t, out_of_place=False):
-                s = torch.from_numpy(((np.sort(self._u(t)) ^ self.f).view(np.int32)).copy())
-                if out_of_place:
-                    return s
-                t.copy_(s)
-                return t
-
-            def merge(self, a, b, d0, d1):
-                cat = np.concatenate([self._u(a), self._u(b)])
-                idx = np.argsort(cat, kind="stable")  # a's elements first on ties
-                return torch.from_numpy(((cat[idx][d0:d1] ^ self.f).view(np.int32)).copy())
-
-            def key_le(self, x, y):
-                f = int(self.f)
-                return ((x & 0xFFFFFFFF) ^ f) <= ((y & 0xFFFFFFFF) ^ f)
-
-        m, dist_name, seed, key = cfg["m"], cfg["dist"], cfg["seed"], cfg["key"]
-        shard = O.gen(m, seed, dist_name, first=rank * m)
-        t = torch.from_numpy(shard.view(np.int32).copy())
-        if cfg.get("exchange") == "splitters":
-            out = D.dist_sort_splitters(t, NumpyOps(key), copy_input=cfg.get("copy", False),
-                                        oversample=cfg.get("oversample", 64))
-        else:
-            out = D.dist_sort(t, NumpyOps(key), partial=cfg["partial"], stride=cfg["stride"],
-                              copy_input=cfg.get("copy", False))
-        if cfg.get("copy", False):
-            assert torch.equal(t, torch.from_numpy(shard.view(np.int32)))  # input untouched
-        q.put((rank, out.numpy().copy()))
+        for ci, cfg in cfgs:
+            q.put((ci, rank, _run_cfg(O, D, rank, world, cfg)))
     finally:
         dist.destroy_process_group()
 
 
-def run(world, cfg):
+def run_all(world, cfgs):
+    """{config index: concatenated ranges} for the (index, config) pairs, checked for
+    range order / global offsets and balance"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, cfg, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, cfgs, q)) for r in range(world)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=180) for _ in range(world))
+    got = {}
+    for _ in range(world * len(cfgs)):
+        ci, r, res = q.get(timeout=300)
+        got[(ci, r)] = res
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    if cfg.get("max_share"):
-        sizes = [res[r].size for r in range(world)]
-        assert max(sizes) <= cfg["max_share"] * cfg["m"], sizes
-    return np.concatenate([res[r] for r in range(world)])
+    out = {}
+    for ci, cfg in cfgs:
+        res = {r: got[(ci, r)][0] for r in range(world)}
+        if got[(ci, 0)][1] is not None:  # splitter exchange: ranges in rank order at their global offsets
+            off = 0
+            for r in range(world):
+                assert got[(ci, r)][1] == off, (ci, r, got[(ci, r)][1], off)
+                off += res[r].size
+        if cfg.get("max_share"):
+            sizes = [res[r].size for r in range(world)]
+            assert max(sizes) <= cfg["max_share"] * cfg["m"], (ci, sizes)
+        out[ci] = np.concatenate([res[r] for r in range(world)])
+    return out
 
 
 CFGS = [
@@ -105,35 +129,57 @@ CFGS = [
     dict(m=3000, dist="mod1000", seed=0x5EED0007, key="u32", partial=False, stride=64),
     dict(m=2000, dist="const", seed=1, key="u32", partial=True, stride=7),
     dict(m=2000, dist="reversed", seed=1, key="u32", partial=True, stride=128),
-    dict(m=5000, dist="u32", seed=0x5EED0008, key="u32", exchange="splitters", copy=True),
+    # the product's splitter schedule (dist_plan.h) on host rank operations
+    dict(m=5000, dist="u32", seed=0x5EED0008, key="u32", exchange="splitters"),
     dict(m=4000, dist="mod100", seed=0x5EED0009, key="u32", exchange="splitters"),
-    dict(m=3001, dist="u32", seed=0x5EED000A, key="i32", exchange="splitters", oversample=3),
+    dict(m=3001, dist="u32", seed=0x5EED000A, key="i32", exchange="splitters"),
     dict(m=100, dist="const", seed=3, key="u32", exchange="splitters"),
     dict(m=1, dist="u32", seed=4, key="u32", exchange="splitters"),
     # repeated keys are cut between ranks by (key, rank, position) splitters: every
     # range stays near its share (a constant input used to land on one rank)
-    dict(m=4000, dist="const", seed=5, key="u32", exchange="splitters", max_share=1.05),
-    dict(m=4000, dist="mod100", seed=6, key="i32", exchange="splitters", max_share=1.05),
+    dict(m=40000, dist="const", seed=5, key="u32", exchange="splitters", max_share=1.02),
+    dict(m=40000, dist="mod100", seed=6, key="i32", exchange="splitters", max_share=1.02),
+    dict(m=20000, dist="sorted", seed=7, key="u32", exchange="splitters", max_share=1.02),
+    dict(m=20000, dist="reversed", seed=8, key="u32", exchange="splitters", max_share=1.02),
+    # ragged and empty shards (the last entries are cut to the world size)
+    dict(m=3000, dist="u32", seed=9, key="u32", exchange="splitters", sizes=[0, 3000, 1, 7000, 0, 5, 2999, 0]),
 ]
 
 
-@pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("ci", range(len(CFGS)))
-def test_dist_sort_gloo(oracle, world, ci):
-    cfg = CFGS[ci]
-    got = run(world, cfg)
-    full = oracle.gen(cfg["m"] * world, cfg["seed"], cfg["dist"])
-    if cfg["dist"] == "reversed":
-        full = np.concatenate([oracle.gen(cfg["m"], cfg["seed"], "reversed", first=r * cfg["m"])
+def _expected(oracle, world, cfg):
+    """the whole array = the shards as the workers generate them, in rank order, sorted"""
+    if cfg.get("exchange") == "splitters":
+        sizes = cfg.get("sizes") or [cfg["m"]] * world
+        full = np.concatenate([oracle.gen(sizes[r], cfg["seed"], cfg["dist"], first=sum(sizes[:r]))
                                for r in range(world)])
-    exp = oracle.sort_i32(full.view(np.int32)).view(np.uint32) if cfg["key"] == "i32" else oracle.sort_u32(full)
-    np.testing.assert_array_equal(got.view(np.uint32), exp)
+    else:
+        full = np.concatenate([oracle.gen(cfg["m"], cfg["seed"], cfg["dist"], first=r * cfg["m"])
+                               for r in range(world)])
+    return oracle.sort_i32(full.view(np.int32)).view(np.uint32) if cfg["key"] == "i32" else oracle.sort_u32(full)
 
 
-@pytest.mark.parametrize("ci", [0, 6, 11, 12])
-def test_dist_sort_gloo_world8(oracle, ci):
-    """BASELINE config 5's rank count (8) on CPU: bitonic network and splitter exchange."""
-    test_dist_sort_gloo(oracle, 8, ci)
+def _check_world(oracle, world, indices):
+    cfgs = []
+    for ci in indices:
+        cfg = dict(CFGS[ci])
+        if cfg.get("sizes"):
+            cfg["sizes"] = cfg["sizes"][:world]
+        cfgs.append((ci, cfg))
+    got = run_all(world, cfgs)
+    for ci, cfg in cfgs:
+        np.testing.assert_array_equal(got[ci].view(np.uint32), _expected(oracle, world, cfg), err_msg=f"config {ci}")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_sort_gloo(oracle, world):
+    """every config: bitonic network (0-5) and the product's splitter schedule (6-15)"""
+    _check_world(oracle, world, range(len(CFGS)))
+
+
+def test_dist_sort_gloo_world8(oracle):
+    """BASELINE config 5's rank count (8) on CPU: bitonic network and the product's
+    splitter schedule."""
+    _check_world(oracle, 8, [0, 6, 11, 12, 13, 15])
 
 
 def test_schedule_shape():

@@ -1,10 +1,14 @@
 """labsort_sort_host_multi / labsort_sort_host_ranks (csrc/multi.hip) on the GPU:
-the whole one-process multi-GPU schedule -- shard H2D, local sorts, splitters, cut
-points, exchange, K-way merge of the received runs, D2H to global offsets -- with
-p ranks sharing cuda:0 and exchanging by peer copies, checked against std::sort (the
-oracle).  The RCCL transport is exercised with one rank (its send to itself goes
-through ncclSend/ncclRecv in a group); its multi-device use needs an 8-GPU node
-(unmeasured on hardware here)."""
+the whole one-process multi-GPU schedule (csrc/dist_plan.h) -- chunked shard H2D under
+the chunk sorts, splitters, cut points, exchange, merge of the received runs, D2H to
+global offsets range by range -- with p ranks sharing cuda:0 and exchanging by peer
+copies, checked against std::sort (the oracle) and, at BASELINE config 5's size (2^30
+keys in 8 ranks), against the SHA-256 fixture.  The RCCL transport's multi-device use
+needs an 8-GPU node (unmeasured on hardware here); ncclCommInitAll with one rank runs."""
+import hashlib
+import json
+import os
+
 import numpy as np
 import pytest
 
@@ -61,3 +65,45 @@ def test_sort_host_multi_arg_checks(ls, torch_gpu):
         ls.sort_host_ranks(a, [0, 0], transport="rccl")  # RCCL: one rank per device
     with pytest.raises(ls.LabsortError):
         ls.sort_host_ranks(a, [0] * 9, transport="peer")  # > LABSORT_MULTI_MAX_RANKS
+
+
+@pytest.mark.parametrize("p", [1, 3, 8])
+@pytest.mark.parametrize("pin", ["0", "1"])
+def test_sort_host_ranks_chunked(ls, oracle, torch_gpu, monkeypatch, p, pin):
+    """Each rank's shard copied and sorted in 8 chunks (LABSORT_HOST_PIPE=1 chunks from
+    2^16 keys per rank), with and without the caller's array page-locked (LABSORT_PIN)."""
+    monkeypatch.setenv("LABSORT_HOST_PIPE", "1")
+    monkeypatch.setenv("LABSORT_PIN", pin)
+    n = p * ((1 << 19) + 77)
+    a = oracle.gen(n, 0x5EED7500 + p, "u32")
+    b = a.copy()
+    ls.sort_host_ranks(b, [0] * p, transport="peer")
+    np.testing.assert_array_equal(b, oracle.sort_u32(a))
+    t, _ = ls.multi_timing()
+    assert t["h2d"] > 0 and t["local_sort"] > 0 and t["total"] > 0
+    assert sum(ls.multi_range_counts(p)) == n
+
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "big.json")
+
+
+def test_config5_2e30_8ranks_one_gpu(ls, torch_gpu):
+    """BASELINE config 5 at full size through its own partition: 2^30 uint32 keys, 8
+    ranks (sharing cuda:0: peer copies stand in for xGMI), chunked H2D per rank,
+    splitters, exchange, merge, ranged D2H; the result matches the fixture word for
+    word and every rank's range is within 2 % of n/8."""
+    torch = torch_gpu
+    c = json.load(open(GOLD))["config5_2^30_u32"]
+    n = 1 << c["log2n"]
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, c["seed"], c["dist"])
+    a = t.cpu().numpy().view(np.uint32)
+    del t
+    torch.cuda.empty_cache()
+    ls.sort_host_ranks(a, [0] * 8, transport="peer")
+    counts = ls.multi_range_counts(8)
+    assert sum(counts) == n and max(counts) <= 1.02 * n / 8, counts
+    assert int(a[0]) == c["first"] and int(a[-1]) == c["last"] and int(a[n // 2]) == c["median"]
+    assert hashlib.sha256(a.tobytes()).hexdigest() == c["sha256_sorted_u32"]
+    ph, sent = ls.multi_timing()
+    print("config5 8 ranks on one GPU:", {k: round(v, 2) for k, v in ph.items()}, "max sent", sent)

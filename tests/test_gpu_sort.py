@@ -250,6 +250,23 @@ def test_sort_pairs(ls, oracle, torch_gpu, n, dist, key, algo):
     np.testing.assert_array_equal(from_dev(tv), ev)
 
 
+@pytest.mark.parametrize("dist", ["u32", "sorted", "reversed"])
+def test_sort_pairs_large(ls, oracle, torch_gpu, dist):
+    """Key/value radix at 2^24 + 5 pairs: the persistent onesweep passes (segmented
+    look-back chains, partial first tiles per segment) carrying the payloads."""
+    torch = torch_gpu
+    n = (1 << 24) + 5
+    k = oracle.gen(n, SEED + 31, dist)
+    v = np.arange(n, dtype=np.uint32)
+    ek, ev = oracle.stable_sort_pairs(k, v, "u32")
+    tk, tv = to_dev(torch, k), to_dev(torch, v)
+    ok, ov = torch.empty_like(tk), torch.empty_like(tv)
+    ls.sort_pairs_device(tk, tv, ok, ov, n, key="u32", algo="radix")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(from_dev(ok), ek)
+    np.testing.assert_array_equal(from_dev(ov), ev)
+
+
 def test_sort_pairs_bad_args(ls, torch_gpu):
     torch = torch_gpu
     t = torch.zeros(1 << 16, dtype=torch.int32, device="cuda")

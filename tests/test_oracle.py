@@ -94,6 +94,20 @@ def test_sort_oracle_big_sha(oracle, big):
             assert sha(oracle.sort_i32(a.view(np.int32))) == c["sha256_sorted_i32"], name
 
 
+def test_config1_cpu_reference_path(ls, oracle, big):
+    """BASELINE config 1 (n=2^16 uniform uint32, the reference's CPU path, no GPU):
+    std::sort (the oracle) and order_with_trust (rocThrust's host sort, lab.cu:404-406,
+    which runs on the CPU: SURVEY F7) both reproduce the committed fixture word for word."""
+    c = big["config1_2^16_u32"]
+    a = oracle.gen(1 << c["log2n"], c["seed"], c["dist"])
+    assert sha(a) == c["sha256_input"]
+    assert sha(oracle.sort_u32(a)) == c["sha256_sorted_u32"]
+    b = a.view(np.int32).copy()
+    ls.order_with_trust(b)  # int32 order, in place
+    assert sha(b) == c["sha256_sorted_i32"]
+    assert int(oracle.sort_u32(a)[0]) == c["first"] and int(oracle.sort_u32(a)[-1]) == c["last"]
+
+
 def test_parallel_sort_matches(oracle):
     a = oracle.gen(1 << 18, 77, "mod1000")
     b = a.copy()
