@@ -87,7 +87,10 @@ def pmc_traffic(kernel_class: str, n: int):
             continue
         k = d.get("kernels", {}).get(kernel_class)
         if k and int(d.get("n", -1)) == n and k.get("hbm_bytes_per_launch"):
-            return float(k["hbm_bytes_per_launch"]), os.path.relpath(f, REPO)
+            how = (f"read x{k['read_factor']} ({k['read_shape']}), write x{k['write_factor']} ({k['write_shape']}) "
+                   "from the pmc_cal calibration" if d.get("calibration") and "read_factor" in k
+                   else "read x2 (guide, 16-B reads), write as measured (uncalibrated)")
+            return float(k["hbm_bytes_per_launch"]), os.path.relpath(f, REPO) + ": " + how
     return None, None
 
 

@@ -5,9 +5,11 @@ set -e
 HERE="$(cd "$(dirname "$0")" && pwd)"
 C="$HERE/../../radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd/csrc"
 mkdir -p "$HERE/libs" "/tmp/lsv_$1"
+pids=()
 for f in kernels kmerge gsweep api multi thrust_host; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -w $2 -c "$C/$f.hip" -o "/tmp/lsv_$1/$f.o" &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait $p || { echo "compile failed ($1)"; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$HERE/libs/liblabsort_$1.so" /tmp/lsv_$1/*.o -ldl -lpthread
 echo "built harness/exp/libs/liblabsort_$1.so"

@@ -216,13 +216,17 @@ int labsort_merge_pass(const void *d_in, void *d_out, size_t n, size_t run, int 
  * d_part: >= labsort_merge_parts(d1-d0) words. */
 int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *d_out, size_t d0, size_t d1,
                   int key_type, uint32_t *d_part, void *stream);
-/* K-way merge of up to 8 sorted runs lying back to back in d_in: run q =
+/* Merge of up to 8 sorted runs lying back to back in d_in: run q =
  * d_in[h_offsets[q] .. h_offsets[q+1]), q < nruns (host array of nruns+1 offsets).
  * Writes the merged keys to d_out[h_offsets[0] .. h_offsets[nruns]) (d_out != d_in);
- * equal keys keep run order (stable).  One pass over HBM (the multi-GPU exchange can
- * merge the p runs it receives with it: HipOps(kway=True); on MI355X the tree of
- * pairwise passes is faster).  Generalises separators_kernel + merge_segments_kernel (lab.cu:209-300)
- * from 2 to K runs.  d_ws: >= labsort_merge_runs_workspace_bytes(h_offsets[nruns]). */
+ * equal keys keep run order (stable).  Default: ceil(log2 nruns) levels of pairwise
+ * merge-path passes over explicit pairs of runs (k_merge_pass_p, one launch per pair),
+ * ping-ponging through the workspace so the last level writes d_out;
+ * LABSORT_MERGE_RUNS=kway: one K-way pass instead (kmerge.hip, slower on MI355X:
+ * DESIGN.md §3.2).  Generalises separators_kernel + merge_segments_kernel
+ * (lab.cu:209-300) from 2 to K runs; the multi-GPU schedule merges the runs a rank
+ * receives with it.  d_ws: >= labsort_merge_runs_workspace_bytes(h_offsets[nruns])
+ * (the larger of the ping-pong keys and the K-way pass's cuts). */
 size_t labsort_merge_runs_workspace_bytes(size_t n);
 int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, int nruns, int key_type,
                        void *d_workspace, size_t ws_bytes, void *stream);

@@ -5,15 +5,19 @@
 Reads  <dir>/prof_<tag>/run_kernel_stats.csv           (--kernel-trace --stats pass)
        <dir>/pmc_FETCH_SIZE_<tag>/run_counter_collection.csv   (separate --pmc pass)
        <dir>/pmc_WRITE_SIZE_<tag>/run_counter_collection.csv   (separate --pmc pass)
+       <dir>/cal_FETCH_SIZE_<tag>/run_counter_collection.csv   (harness/bin/pmc_cal, optional)
+       <dir>/cal_WRITE_SIZE_<tag>/run_counter_collection.csv
 Writes profiles/<tag>_kernel_stats.csv (copy of the stats summary) and
        profiles/<tag>_pmc.json: per labsort kernel class, average FETCH_SIZE and
        WRITE_SIZE per launch and the corrected HBM bytes per launch.
 
-Correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE and WRITE_SIZE are in KiB;
-on gfx950 FETCH_SIZE reports exactly half the bytes of a wide coalesced
-streaming read, so read bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE is exact for
-16-B streaming stores (our scatter stores are 4 B per lane: uncalibrated, so
-the write side is reported as measured).  Infinity-Cache hits are counted.
+Correction.  FETCH_SIZE and WRITE_SIZE are in KiB.  MI355X_MICROARCH.md §HBM calibrates
+only the 16-B/lane streaming read (FETCH_SIZE = 1/2 of the bytes); the labsort kernels
+use 4-B/lane loads and stores, so harness/exp/pmc_cal.hip moves a known 1 GiB with each
+access shape the product uses and this script derives a factor per shape
+(bytes / counter bytes).  Each product kernel class is corrected by the factors of its
+own load and store shapes (SHAPES); without a calibration pass the guide's x2 read /
+x1 write rule is used and the summary says so.  Infinity-Cache hits are counted.
 """
 import csv
 import json
@@ -36,9 +40,14 @@ def klass(name):
 
 
 def read_pmc(path, counter):
+    """average counter value per launch and kernel class, over `path` and, if present, the
+    merge-bench pass beside it (<dir>_merge)"""
     acc = {}
-    with open(path) as f:
-        for row in csv.DictReader(f):
+    paths = [path] + [p for p in [path.replace(os.sep + "run_counter", "_merge" + os.sep + "run_counter")]
+                      if p != path and os.path.exists(p)]
+    rows = [row for p in paths for row in csv.DictReader(open(p))]
+    if True:
+        for row in rows:
             if row["Counter_Name"] != counter:
                 continue
             c = klass(row["Kernel_Name"])
@@ -50,25 +59,75 @@ def read_pmc(path, counter):
     return {c: v[0] / v[1] for c, v in acc.items() if v[1]}
 
 
+# access shapes of each kernel class (the instructions in its ISA): read, write
+SHAPES = {"onesweep": ("cal_rd_buf_nt", "cal_wr_buf"),      # buffer_load_dword nt / buffer_store_dword
+          "histogram": ("cal_rd_x4_nt", None),                # global_load_dwordx4 nt (k_hist_seg)
+          "merge": ("cal_rd_dword", "cal_wr_x4"),             # global_load_dword / global_store_dwordx4
+          "tile_sort": ("cal_rd_dword", "cal_wr_dword"),      # global_load_dword / global_store_dword
+          "count_descents": ("cal_rd_dword", None),           # global_load_dword (a check: 1 GiB read)
+          "fill": (None, "cal_wr_dword")}                     # global_store_dword (a check: 1 GiB written)
+CAL_BYTES = float(1 << 30)  # every calibration kernel moves 2^28 words per launch
+
+
+def calibration(d, tag):
+    """{shape: bytes per counter byte} from the pmc_cal passes, or None"""
+    f = os.path.join(d, f"cal_FETCH_SIZE_{tag}", "run_counter_collection.csv")
+    w = os.path.join(d, f"cal_WRITE_SIZE_{tag}", "run_counter_collection.csv")
+    if not (os.path.exists(f) and os.path.exists(w)):
+        return None
+
+    def per_kernel(path, counter):
+        acc = {}
+        for row in csv.DictReader(open(path)):
+            if row["Counter_Name"] != counter or not row["Kernel_Name"].startswith("cal_"):
+                continue
+            k = row["Kernel_Name"].split("(")[0]
+            a = acc.setdefault(k, [0.0, 0])
+            a[0] += float(row["Counter_Value"])
+            a[1] += 1
+        return {k: v[0] / v[1] for k, v in acc.items()}
+
+    fetch, write = per_kernel(f, "FETCH_SIZE"), per_kernel(w, "WRITE_SIZE")
+    cal = {}
+    for k, kib in fetch.items():
+        if k.startswith("cal_rd") and kib > 0:
+            cal[k] = {"counter_kib": round(kib, 1), "factor": CAL_BYTES / (kib * 1024)}
+    for k, kib in write.items():
+        if k.startswith("cal_wr") and kib > 0:
+            cal[k] = {"counter_kib": round(kib, 1), "factor": CAL_BYTES / (kib * 1024)}
+    return cal
+
+
 def main():
     d, tag = sys.argv[1], sys.argv[2]
     n = int(sys.argv[sys.argv.index("--n") + 1]) if "--n" in sys.argv else 1 << 28
     here = os.path.dirname(os.path.abspath(__file__))
-    stats = os.path.join(d, f"prof_{tag}", "run_kernel_stats.csv")
-    if os.path.exists(stats):
-        shutil.copy(stats, os.path.join(here, f"{tag}_kernel_stats.csv"))
+    for leg in ("", "_merge"):
+        stats = os.path.join(d, f"prof_{tag}{leg}", "run_kernel_stats.csv")
+        if os.path.exists(stats):
+            shutil.copy(stats, os.path.join(here, f"{tag}{leg}_kernel_stats.csv"))
     fetch = read_pmc(os.path.join(d, f"pmc_FETCH_SIZE_{tag}", "run_counter_collection.csv"), "FETCH_SIZE")
     write = read_pmc(os.path.join(d, f"pmc_WRITE_SIZE_{tag}", "run_counter_collection.csv"), "WRITE_SIZE")
+    cal = calibration(d, tag)
     out = {"tag": tag, "n": n, "units": "bytes per launch",
-           "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB as measured",
-           "kernels": {}}
+           "correction": ("per access shape from harness/exp/pmc_cal.hip (calibration below): read = FETCH_SIZE "
+                          "x factor(read shape), write = WRITE_SIZE x factor(write shape)") if cal else
+                         "read = 2 x FETCH_SIZE KiB (gfx950 half-count, 16-B reads), write = WRITE_SIZE KiB as measured "
+                         "(uncalibrated)",
+           "calibration": cal, "kernels": {}}
     for c in sorted(set(fetch) | set(write)):
         f, w = fetch.get(c, 0.0), write.get(c, 0.0)
+        rs, ws = SHAPES.get(c, (None, None))
+        fr = cal[rs]["factor"] if cal and rs in cal else 2.0
+        fw = cal[ws]["factor"] if cal and ws in cal else 1.0
         out["kernels"][c] = {"fetch_size_kib": round(f, 1), "write_size_kib": round(w, 1),
-                             "read_bytes": 2 * f * 1024, "write_bytes": w * 1024,
-                             "hbm_bytes_per_launch": 2 * f * 1024 + w * 1024,
+                             "read_shape": rs, "write_shape": ws, "read_factor": round(fr, 4),
+                             "write_factor": round(fw, 4),
+                             "read_bytes": fr * f * 1024, "write_bytes": fw * w * 1024,
+                             "hbm_bytes_per_launch": fr * f * 1024 + fw * w * 1024,
                              "algorithmic_bytes_per_launch": {"onesweep": 8 * n, "histogram": 4 * n,
-                                                              "merge": 8 * n, "tile_sort": 8 * n}.get(c)}
+                                                              "merge": 8 * n, "tile_sort": 8 * n,
+                                                              "count_descents": 4 * n, "fill": 4 * n}.get(c)}
     with open(os.path.join(here, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out["kernels"].get("onesweep"), indent=1))

@@ -93,12 +93,14 @@ struct RadixLayout {
         off_segplan, total;
 };
 
-RadixLayout radix_layout(size_t n, int bits) {
+// `tile`: keys per look-back slot of the pass kernel that will run (OSP_TILE for the
+// persistent k_onesweep_p, OS_TILE for the non-persistent k_onesweep)
+RadixLayout radix_layout(size_t n, int bits, size_t tile) {
     RadixLayout L{};
     L.bits = bits;
     L.R = 1 << bits;
     L.P = (32 + bits - 1) / bits;
-    L.ntiles = (n + OS_TILE - 1) / OS_TILE + (bits == 8 ? NSEG : 0);
+    L.ntiles = (n + tile - 1) / tile + (bits == 8 ? NSEG : 0);
     // zeroed block: err | hist | segment histograms | counters | lookback.  The device
     // error word is the workspace's first word (labsort_workspace_status reads it).
     size_t o = 0;
@@ -179,7 +181,7 @@ void hook_end(void *ctx, int cls, hipStream_t s) {
 bool small_path(size_t n, int algo) { return algo != LABSORT_ALGO_RADIX1 && n <= (size_t)TS_TILE; }
 
 int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int bits, char *ws, hipStream_t s) {
-    const RadixLayout L = radix_layout(n, bits);
+    const RadixLayout L = radix_layout(n, bits, bits == 8 ? OSP_TILE : OS_TILE);
     Bufs b;
     b.p[SEL_IN] = const_cast<uint32_t *>(in);
     b.p[SEL_OUT] = out;
@@ -416,12 +418,11 @@ size_t labsort_workspace_bytes(size_t n, int algo) {
     algo = resolve_algo(algo, n);
     if (small_path(n, algo)) return 256;
     switch (algo) {
-    case LABSORT_ALGO_RADIX: {
-        const size_t r = radix_layout(n, 8).total;
-        const size_t g = gs_layout(n).total;
-        return r > g ? r : g;  // either implementation fits (LABSORT_RADIX_IMPL may change)
-    }
-    case LABSORT_ALGO_RADIX1: return radix_layout(n, 1).total;
+    // the implementation that will run (use_gather reads LABSORT_RADIX_IMPL; a sort run
+    // after that variable changes is checked against the same function: ERR_ARG if the
+    // caller's workspace was sized for the other one)
+    case LABSORT_ALGO_RADIX: return use_gather(n) ? gs_layout(n).total : radix_layout(n, 8, OSP_TILE).total;
+    case LABSORT_ALGO_RADIX1: return radix_layout(n, 1, OS_TILE).total;
     case LABSORT_ALGO_MERGE: return merge_layout(n).total;
     default: return 0;
     }
@@ -714,10 +715,22 @@ int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, i
 
 size_t labsort_pair_tile_keys(void) { return (size_t)TS_TILE_KV; }
 
+namespace {
+// key/value radix: the persistent onesweep passes unless LABSORT_PAIRS_OSP=0 selects
+// the non-persistent ones (8192-key look-back slots)
+bool pairs_persistent() {
+    const char *e = std::getenv("LABSORT_PAIRS_OSP");
+    return !(e && !std::strcmp(e, "0"));
+}
+size_t pairs_tile() { return pairs_persistent() ? (size_t)OSP_TILE : (size_t)OS_TILE; }
+}  // namespace
+
 size_t labsort_pairs_workspace_bytes(size_t n, int algo) {
     if (n <= (size_t)TS_TILE_KV) return 256;
+    algo = resolve_algo(algo, n);
     if (algo == LABSORT_ALGO_MERGE) return align_up(n * 4, 256) * 2;  // ping-pong keys | payloads
-    return align_up(radix_layout(n, 8).total, 256) + align_up(n * 4, 256);  // radix workspace | payload ping-pong
+    // radix workspace | payload ping-pong
+    return align_up(radix_layout(n, 8, pairs_tile()).total, 256) + align_up(n * 4, 256);
 }
 
 namespace {
@@ -725,14 +738,9 @@ namespace {
 // then the persistent onesweep passes carrying each payload with its key
 // (k_onesweep_p<..., KV>), the final copy of keys and payloads under the same buffer
 // plan.  LABSORT_PAIRS_OSP=0: the non-persistent key/value pass (k_onesweep<8, ..., KV>).
-bool pairs_persistent() {
-    const char *e = std::getenv("LABSORT_PAIRS_OSP");
-    return !(e && !std::strcmp(e, "0"));
-}
-
 int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint32_t *vo, size_t n, uint32_t flip,
                      char *ws, hipStream_t s) {
-    const RadixLayout L = radix_layout(n, 8);
+    const RadixLayout L = radix_layout(n, 8, pairs_tile());
     Bufs b, vb;
     b.p[SEL_IN] = const_cast<uint32_t *>(ki);
     b.p[SEL_OUT] = ko;
@@ -891,9 +899,11 @@ void sort(int *in, int n) {
                             : labsort_sort_host(in, (size_t)n, LABSORT_KEY_I32, default_algo());
     if (st != LABSORT_OK) {
         const int hip = gpus > 1 ? labsort_multi_last_hip_error() : g_last_hip;
-        std::fprintf(stderr, "GPUassert: %s %s %d\n",
-                     st == LABSORT_ERR_HIP ? hipGetErrorString((hipError_t)hip) : labsort_error_string(st), __FILE__,
-                     __LINE__);
+        // the multi-GPU path records what failed (HIP call, RCCL result) in words
+        const char *what = gpus > 1 && *labsort_multi_error_detail() ? labsort_multi_error_detail()
+                           : st == LABSORT_ERR_HIP                      ? hipGetErrorString((hipError_t)hip)
+                                                                        : labsort_error_string(st);
+        std::fprintf(stderr, "GPUassert: %s %s %d\n", what, __FILE__, __LINE__);
         std::exit(st == LABSORT_ERR_HIP && hip ? hip : 1);
     }
     if (verify) verify_or_exit("order_array", in, (size_t)n, before);

@@ -349,7 +349,7 @@ __device__ void build_segplan(SegPlan *__restrict__ sp, const uint32_t *__restri
             sp->tpre[s] = tp;
             if (s < NSEG) {
                 // tiles aligned to OSP_TILE boundaries (k_onesweep_p's tile_range)
-                const uint32_t a0 = start[s] & ~((uint32_t)OSP_TILE - 1u);
+                const uint32_t a0 = start[s] - start[s] % (uint32_t)OSP_TILE;
                 const uint32_t ts = start[s + 1] > start[s] ? (start[s + 1] - a0 + OSP_TILE - 1) / OSP_TILE : 0u;
                 tp += ts;
                 mx = ts > mx ? ts : mx;
@@ -719,7 +719,7 @@ struct OspSmem {
     uint32_t keys[TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0)];  // padded: see osp_pad
     uint32_t vals[KV ? TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0) : 1];  // key/value: payloads, reordered alike
     uint32_t wh[W * R];
-    uint64_t match[MATCH && !KV ? W * R : 1];
+    uint64_t match[MATCH && !KV && OSP_KPT <= 16 ? W * R : 1];  // (no room beside bigger tiles)
     uint32_t probe[WAVE];
     uint32_t ordered;
     uint32_t hist[R];
@@ -841,7 +841,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     // wave loads): a segment's first tile runs from its start to the next boundary.
     auto tile_range = [&](uint32_t c, uint32_t &beg, uint32_t &nvalid) {
         const uint32_t sg = c & segmask, l = c >> segbits;
-        const uint32_t s0 = sm.start[sg], a0 = s0 & ~((uint32_t)TILE - 1u);
+        const uint32_t s0 = sm.start[sg], a0 = s0 - s0 % (uint32_t)TILE;
         beg = l ? a0 + l * (uint32_t)TILE : s0;
         const uint32_t tend = a0 + (l + 1u) * (uint32_t)TILE, send = sm.start[sg + 1];
         nvalid = (tend < send ? tend : send) - beg;
@@ -956,7 +956,8 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                     const uint32_t r = wave_atomic_rank(wh, d, lane);
                     rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
                 } else {
-                    const uint64_t m = (RANK != OSP_RANK_BALLOT && !KV) ? lds_peers(wm + d, lane) : match8(d);
+                    const uint64_t m = (RANK != OSP_RANK_BALLOT && !KV && OSP_KPT <= 16) ? lds_peers(wm + d, lane)
+                                                                                          : match8(d);
                     const uint32_t pre = mbcnt64(m);
                     const uint32_t old = wh[d];
                     if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
@@ -1704,9 +1705,12 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
         variant = (e && e[0] >= '0' && e[0] <= '2' && e[1]) ? ((e[0] - '0') << 1) | (e[1] == '1') : OSP_DEFAULT_VARIANT;
     }
     if (vb) {  // key/value: the default variant (lane-ordered atomic rank) only
-        k_onesweep_p<2, false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter,
-                                                             err, *vb);
-        return hipGetLastError();
+        if constexpr (OSP_KPT <= 16) {  // keys + payloads in LDS: 16384-pair tiles at most
+            k_onesweep_p<2, false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback,
+                                                                 counter, err, *vb);
+            return hipGetLastError();
+        }
+        return hipErrorInvalidValue;
     }
     switch (variant) {
     case 0: k_onesweep_p<0, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;

@@ -91,11 +91,13 @@ def test_sizes_and_limits(ls):
         assert ls.workspace_bytes(n, "auto") == ls.workspace_bytes(n, "merge")
     for n in ((1 << 18) + 1, 1 << 20, 1 << 22, 1 << 28, (1 << 30) - 1):
         assert ls.workspace_bytes(n, "auto") == ls.workspace_bytes(n, "radix")
-    # radix at 2^28 fits either implementation: the gathered passes' two key buffers and
-    # run tables (2 x 4n + ~200 MB) or the onesweep tmp keys + look-back words
-    w = ls.workspace_bytes(1 << 28, "radix")
-    assert w >= 4 * (1 << 28) + 4 * 32768 * 256 * 4 and w >= 8 * (1 << 28)
-    assert w < 8 * (1 << 28) + (256 << 20)
+    # radix is sized for the implementation that runs: at 2^28 the onesweep
+    # passes' ping-pong keys + 4 passes of look-back words (one slot of 256 digits per
+    # 16384-key tile); at 2^20 the gathered passes' two key buffers and run tables
+    n = 1 << 28
+    w = ls.workspace_bytes(n, "radix")
+    assert w >= 4 * n + 4 * (n // 16384) * 256 * 4 and w < 4 * n + (128 << 20)
+    assert ls.workspace_bytes(1 << 20, "radix") >= 8 * (1 << 20)
 
 
 def test_argument_errors(ls):
