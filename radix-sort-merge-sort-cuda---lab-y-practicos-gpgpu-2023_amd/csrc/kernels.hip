@@ -755,7 +755,18 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                                                           uint32_t *lookback, uint32_t *counter, uint32_t *err,
                                                           Bufs vbufs) {
     using S = OspSmem<RANK != OSP_RANK_BALLOT, KV>;
-    constexpr bool PF = OSP_PREFETCH && !KV;  // next tile's keys loaded one iteration ahead
+#ifndef LABSORT_OSP_KV_PF
+#define LABSORT_OSP_KV_PF 0  // r26 A/B at 2^28 pairs: 0.830 ms per pass without, 1.018 with (27 VGPRs spilled)
+#endif
+    // next tile's keys loaded one iteration ahead (key/value: the keys only; B's payloads
+    // are loaded at the top of B's iteration, and first used by B's reorder)
+    constexpr bool PF = OSP_PREFETCH && (!KV || LABSORT_OSP_KV_PF);
+#ifndef LABSORT_OSP_KV_LDSV
+#define LABSORT_OSP_KV_LDSV 0  // r26: 0.843 ms per pass with, 0.830 without
+#endif
+    // key/value: A's payloads are scattered straight from the LDS reorder buffer (they
+    // stay there until B's reorder, after barrier 3), not held in 16 VGPRs
+    constexpr bool LDSV = KV && LABSORT_OSP_KV_LDSV;
     constexpr bool LBASE = OSP_BUF && !KV;    // bases table in LDS
     static_assert(!KV || OSP_BUF, "key/value passes use the buffer-descriptor loads and stores");
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW, LBW2 = OSP_LBW2;
@@ -827,7 +838,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     // carried state of tile A (slot = look-back slot, lo = slot of its segment's first tile)
     uint32_t slotA = OSP_DONE, loA = 0, segA = 0, nvalidA = 0;
     uint32_t kA[KPT];
-    uint32_t vA[KV ? KPT : 1];  // key/value: A's payloads in scatter order
+    uint32_t vA[KV ? KPT : 1];  // key/value: A's payloads in scatter order (unless LDSV)
     uint32_t lwA[LBW];
     uint32_t aggA = 0, dstartA = 0;
     uint32_t *wh = sm.wh + wid * R;
@@ -924,6 +935,8 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         }
         if constexpr (PF) {
             if (cC != OSP_DONE) load_tile(cC, kN);
+            if constexpr (KV)
+                if (haveB) load_vals(cB, vB);
         } else if (haveB) {
             load_tile(cB, kB);
             if constexpr (KV) load_vals(cB, vB);
@@ -1050,7 +1063,8 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                     // a partial tile's sentinels (i >= nvalidA) go past the array's end: dropped
                     const uint32_t dst = i < nvalidA ? sm.delta[((key ^ flip) >> shift) & 255u] + i : n;
                     __builtin_amdgcn_raw_buffer_store_b32(key, rout, dst * 4u, 0, (LABSORT_OSP_NT & 1) ? 2 : 0);
-                    if constexpr (KV) __builtin_amdgcn_raw_buffer_store_b32(vA[j], rvout, dst * 4u, 0, 0);
+                    if constexpr (KV)
+                        __builtin_amdgcn_raw_buffer_store_b32(LDSV ? sm.vals[osp_pad(i)] : vA[j], rvout, dst * 4u, 0, 0);
                 }
             } else if (nvalidA == (uint32_t)TILE) {
 #pragma unroll
@@ -1104,7 +1118,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
 #pragma unroll
             for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * OSP_BLOCK + tid)];
         }
-        if constexpr (KV) {
+        if constexpr (KV && !LDSV) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) vA[j] = sm.vals[osp_pad(j * OSP_BLOCK + tid)];
         }
