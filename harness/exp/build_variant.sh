@@ -6,7 +6,8 @@ HERE="$(cd "$(dirname "$0")" && pwd)"
 C="$HERE/../../radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd/csrc"
 mkdir -p "$HERE/libs" "/tmp/lsv_$1"
 pids=()
-for f in kernels kmerge gsweep api multi thrust_host; do
+SRCS=$(sed -n "s/^SRCS := //p" "$C/Makefile" | sed "s/\.hip//g")  # the product sources
+for f in $SRCS; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -w $2 -c "$C/$f.hip" -o "/tmp/lsv_$1/$f.o" &
   pids+=($!)
 done

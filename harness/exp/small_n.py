@@ -16,7 +16,14 @@ for n in [int(x) for x in os.environ.get("NS", "").split()] or [256, 4096, 32768
     ls.fill(d, n, 0x5EED0002, "u32")
     o = torch.empty_like(d)
     row = {"n": n}
-    for algo in ["radix", "merge"]:
+    ref = torch.sort(d.to(torch.int64) & 0xFFFFFFFF)[0].to(torch.int32)
+    for name in os.environ.get("IMPLS", "radix merge").split():
+        # radix:<impl> selects LABSORT_RADIX_IMPL (small | gather | onesweep)
+        algo, _, impl = name.partition(":")
+        if impl:
+            os.environ["LABSORT_RADIX_IMPL"] = impl
+        else:
+            os.environ.pop("LABSORT_RADIX_IMPL", None)
         ws = torch.empty(max(ls.workspace_bytes(n, algo), 256), dtype=torch.uint8, device="cuda")
         for _ in range(3):
             ls.sort_device(d, o, n, algo=algo, workspace=ws)
@@ -29,5 +36,7 @@ for n in [int(x) for x in os.environ.get("NS", "").split()] or [256, 4096, 32768
             b.synchronize()
             ts.append(a.elapsed_time(b))
         ts.sort()
-        row[algo + "_ms"] = round(ts[len(ts) // 2], 4)
+        ls.workspace_status(ws, n, algo)
+        assert torch.equal(o, ref), (n, name)
+        row[name + "_ms"] = round(ts[len(ts) // 2], 4)
     print(json.dumps(row), flush=True)

@@ -43,7 +43,8 @@ extern "C" {
 /* algorithms */
 #define LABSORT_ALGO_RADIX 0     /* LSD radix, 8-bit digits: gathered passes for 2^16 <= n < 2^26,
                                     onesweep scatter passes outside (LABSORT_RADIX_IMPL=onesweep or
-                                    =gather forces one) */
+                                    =gather forces one; =small: one cooperative launch for
+                                    labsort_tile_keys() < n <= 2^22, small.hip) */
 #define LABSORT_ALGO_MERGE 1     /* LDS tile radix + merge-path merge passes */
 #define LABSORT_ALGO_RADIX1 2    /* LSD radix with 1-bit digits: letra.pdf's split, 32 passes */
 #define LABSORT_ALGO_AUTO 3      /* MERGE for n <= LABSORT_AUTO_MERGE_MAX_KEYS (fewer launches and
@@ -75,7 +76,8 @@ extern "C" {
 #define LABSORT_K_PARTITION 4
 #define LABSORT_K_GSWEEP 5       /* gathered radix pass (LABSORT_ALGO_RADIX, 2^16 <= n < 2^26) */
 #define LABSORT_K_GCOPY 6        /* its final gathered copy */
-#define LABSORT_K_COUNT 7
+#define LABSORT_K_SMALL 7        /* single-launch radix sort (LABSORT_ALGO_RADIX, n <= 2^22) */
+#define LABSORT_K_COUNT 8
 
 /* ---- library info ---- */
 const char *labsort_version(void);

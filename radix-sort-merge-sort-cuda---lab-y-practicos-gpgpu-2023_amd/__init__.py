@@ -30,7 +30,8 @@ OK, ERR_ARG, ERR_HIP, ERR_DEVICE = 0, 1, 2, 3
 ALGO = {"radix": 0, "merge": 1, "radix1": 2, "auto": 3}
 KEY = {"u32": 0, "i32": 1}
 DIST = {"u32": 0, "u31": 1, "mod100": 2, "mod1000": 3, "sorted": 4, "reversed": 5, "const": 6, "lowbits": 7}
-KCLASS = {"histogram": 0, "onesweep": 1, "tile_sort": 2, "merge": 3, "partition": 4, "gsweep": 5, "gcopy": 6}
+KCLASS = {"histogram": 0, "onesweep": 1, "tile_sort": 2, "merge": 3, "partition": 4, "gsweep": 5, "gcopy": 6,
+          "small": 7}
 
 # exported symbols of include/labsort.h + lab.h (checked by tests/test_abi.py)
 C_SYMBOLS = [
@@ -375,14 +376,18 @@ def workspace_bytes(n: int, algo: str = "radix") -> int:
 
 
 GS_MIN_N, GS_MAX_N = 1 << 16, 1 << 26  # LABSORT_ALGO_RADIX's gathered-pass window (common.h)
+SR_MAX_N = 1 << 22  # single-launch radix up to here (common.h SR_MAX_N)
 
 
 def radix_impl(n: int) -> str:
-    """Which LSD implementation LABSORT_ALGO_RADIX runs for n keys: "gather" (gsweep.hip)
-    or "onesweep" (kernels.hip), as api.hip's use_gather decides."""
+    """Which LSD implementation LABSORT_ALGO_RADIX runs for n keys: "gather" (gsweep.hip),
+    "onesweep" (kernels.hip) or, with LABSORT_RADIX_IMPL=small and tile_keys() < n <= 2^22,
+    "small" (small.hip), as api.hip's use_small / use_gather decide."""
     env = os.environ.get("LABSORT_RADIX_IMPL", "")
     if env == "gather":
         return "gather"
+    if tile_keys() < n <= SR_MAX_N and env == "small":
+        return "small"
     if GS_MIN_N <= n < GS_MAX_N and env != "onesweep":
         return "gather"
     return "onesweep"

@@ -147,11 +147,20 @@ MergeLayout merge_layout(size_t n) {
 
 // LABSORT_ALGO_RADIX from GS_MIN_N keys on: the gathered passes (gsweep.hip), unless
 // LABSORT_RADIX_IMPL=onesweep selects the scatter passes (kernels.hip k_onesweep_p)
+bool use_small(size_t n);
 bool use_gather(size_t n) {
     const char *e = std::getenv("LABSORT_RADIX_IMPL");
     if (e && !std::strcmp(e, "gather")) return true;  // any n (experiments, tests)
-    if (n < GS_MIN_N || n >= GS_MAX_N) return false;
+    if (n < GS_MIN_N || n >= GS_MAX_N || use_small(n)) return false;
     return !(e && !std::strcmp(e, "onesweep"));
+}
+// LABSORT_RADIX_IMPL=small, TS_TILE < n <= SR_MAX_N: the single-launch sort (small.hip).
+// Not the default: at 2^20 it measured 0.094 ms (cooperative launch) against 0.082 for
+// the gathered passes
+bool use_small(size_t n) {
+    if (n <= (size_t)TS_TILE || n > SR_MAX_N) return false;
+    const char *e = std::getenv("LABSORT_RADIX_IMPL");
+    return e && !std::strcmp(e, "small");
 }
 
 // GsHooks callbacks: the same event pairs as TimingScope
@@ -421,7 +430,8 @@ size_t labsort_workspace_bytes(size_t n, int algo) {
     // the implementation that will run (use_gather reads LABSORT_RADIX_IMPL; a sort run
     // after that variable changes is checked against the same function: ERR_ARG if the
     // caller's workspace was sized for the other one)
-    case LABSORT_ALGO_RADIX: return use_gather(n) ? gs_layout(n).total : radix_layout(n, 8, OSP_TILE).total;
+    case LABSORT_ALGO_RADIX:
+        return use_small(n) ? sr_layout(n).total : use_gather(n) ? gs_layout(n).total : radix_layout(n, 8, OSP_TILE).total;
     case LABSORT_ALGO_RADIX1: return radix_layout(n, 1, OS_TILE).total;
     case LABSORT_ALGO_MERGE: return merge_layout(n).total;
     default: return 0;
@@ -450,6 +460,11 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
     }
     char *ws = static_cast<char *>(d_ws);
     if (algo == LABSORT_ALGO_MERGE) return sort_merge(in, out, n, flip, ws, s);
+    if (algo == LABSORT_ALGO_RADIX && use_small(n)) {
+        TimingScope ts(LABSORT_K_SMALL, s);
+        HIP_TRY(launch_small_radix(in, out, n, flip, ws, s));
+        return LABSORT_OK;
+    }
     if (algo == LABSORT_ALGO_RADIX && use_gather(n)) {
         HookCtx hc;
         HIP_TRY(launch_gsweep_sort(in, out, n, flip, ws, s, GsHooks{&hc, hook_begin, hook_end}));

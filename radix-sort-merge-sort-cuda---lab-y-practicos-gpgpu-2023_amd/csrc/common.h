@@ -218,6 +218,17 @@ struct GsHooks {
 hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s,
                               const GsHooks &hooks);
 
+// ---- single-launch LSD radix for small arrays (small.hip): one cooperative launch,
+// one 16384-key tile per workgroup, grid barriers between phases ----
+constexpr int SR_BLOCK = 1024, SR_KPT = 16;
+constexpr int SR_TILE = SR_BLOCK * SR_KPT;
+constexpr size_t SR_MAX_N = (size_t)256 * SR_TILE;  // one co-resident workgroup per CU (2^22 keys)
+struct SrLayout {
+    size_t off_err, off_bar, off_andor, off_cnt, off_tmp, total;
+};
+SrLayout sr_layout(size_t n);
+hipError_t launch_small_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s);
+
 constexpr int MAX_PASSES = 32;
 constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_SKIP = 0xFFu;
 constexpr uint32_t NEXT_NONE = 0xFFFFFFFFu;

@@ -1169,146 +1169,176 @@ struct TsSmem {
 
 // KV: key/value pairs (vin/vout, 4-byte payloads); the sort is stable, so equal keys
 // keep their input order and their payloads with them.
+// TS_PERSIST: one workgroup per CU loops over tiles (grid = CUs), so a tile's stores
+// drain while the next tile loads; TS_PFK > 0 also loads the first TS_PFK keys per
+// lane of the workgroup's next tile before its current tile's last pass.
+#ifndef LABSORT_TS_PERSIST
+#define LABSORT_TS_PERSIST 0
+#endif
+#ifndef LABSORT_TS_PFK
+#define LABSORT_TS_PFK 0
+#endif
 template <int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint32_t *out, const uint32_t *vin,
                                                          uint32_t *vout, uint32_t n, uint32_t flip) {
     using S = TsSmem<BLOCK, KPT, KV>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE;
+    constexpr int PFK = KV ? 0 : (LABSORT_TS_PFK < KPT ? LABSORT_TS_PFK : KPT);
     __shared__ S sm;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t base = blockIdx.x * (uint32_t)TILE;
     const uint32_t sentinel = ~flip;
-    const uint32_t wbase = base + wid * (KPT * WAVE) + lane;
-
-    uint32_t k[KPT];
-    uint32_t v[KV ? KPT : 1];
-    uint32_t a = ~0u, o = 0u;
-    const bool full = base + (uint32_t)TILE <= n;  // no bounds checks (one base address)
-    if constexpr (KV) {
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t idx = wbase + j * WAVE;
-            v[j] = idx < n ? vin[idx] : 0u;
-        }
-    }
-    if (full) {
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = ld_stream<NT_TILE>(in + wbase + j * WAVE);
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            a &= k[j] ^ flip;
-            o |= k[j] ^ flip;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t idx = wbase + j * WAVE;
-            const bool ok = idx < n;
-            k[j] = ok ? ld_stream<NT_TILE>(in + idx) : sentinel;
-            const uint32_t x = k[j] ^ flip;
-            a &= ok ? x : ~0u;
-            o |= ok ? x : 0u;
-        }
-    }
-    // bits on which the tile's keys differ -> passes that are not the identity
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        a &= __shfl_xor(a, off);
-        o |= __shfl_xor(o, off);
-    }
-    if (lane == 0) {
-        sm.red_and[wid] = a;
-        sm.red_or[wid] = o;
-    }
+    const uint32_t ntiles = (n + (uint32_t)TILE - 1u) / (uint32_t)TILE;
     if (wid == 0) {  // lane-ordered LDS atomics (see k_onesweep_p): rank by one atomic per key
         const bool ord = lds_lane_ordered(sm.probe, lane);
         if (lane == 0) sm.ordered = ord ? 1u : 0u;
     }
-    __syncthreads();
-    const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
-    uint32_t diff = 0;
-    {
-        uint32_t aa = ~0u, oo = 0u;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            aa &= sm.red_and[w];
-            oo |= sm.red_or[w];
-        }
-        diff = aa ^ oo;
-    }
-    uint32_t *wh = sm.whist + wid * R;
-    for (int pass = 0; pass < 4; ++pass) {
-        const uint32_t shift = pass * 8;
-        if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the block
-        for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
-        uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            // stable wave rank: lane-ordered returning atomic, else peers by 8 ballots
-            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-            uint32_t r;
-            if (atomic_rank) {
-                r = wave_atomic_rank(wh, d, lane);
-            } else {
-                const uint64_t m = match8(d);
-                const uint32_t pre = mbcnt64(m);
-                const uint32_t old = wh[d];
-                if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
-                r = old + pre;
-            }
-            rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
-        }
-        __syncthreads();
-        // tile-wide digit offsets folded into the per-wave offsets: the reorder then
-        // reads one LDS word per key instead of two (LDS was busy 68 % of the kernel,
-        // 60 % of it bank conflicts: profiles/r17_pmc_tile_sort.txt)
-        uint32_t tot = 0;
-        if (tid < (uint32_t)R) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) tot += sm.whist[w * R + tid];
-        }
-        const uint32_t ds = block_excl_scan<BLOCK, R>(tot, sm.wsum);
-        if (tid < (uint32_t)R) {
-            uint32_t run = ds;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint32_t c = sm.whist[w * R + tid];
-                sm.whist[w * R + tid] = run;
-                run += c;
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-            const uint32_t dst = wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
-            sm.keys[dst] = k[j];
-            if constexpr (KV) sm.vals[dst] = v[j];
-        }
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
+    uint32_t pf[PFK ? PFK : 1];
+    bool have_pf = false;
+    for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
+        const uint32_t base = tb * (uint32_t)TILE;
+        const uint32_t wbase = base + wid * (KPT * WAVE) + lane;
+        uint32_t k[KPT];
+        uint32_t v[KV ? KPT : 1];
+        uint32_t a = ~0u, o = 0u;
+        const bool full = base + (uint32_t)TILE <= n;  // no bounds checks (one base address)
         if constexpr (KV) {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) v[j] = sm.vals[wid * (KPT * WAVE) + j * WAVE + lane];
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t idx = wbase + j * WAVE;
+                v[j] = idx < n ? vin[idx] : 0u;
+            }
         }
-    }
-    if (full) {
+        if (full) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
-    } else {
+            for (int j = 0; j < KPT; ++j)
+                k[j] = (j < PFK && have_pf) ? pf[j < PFK ? j : 0] : ld_stream<NT_TILE>(in + wbase + j * WAVE);
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t idx = wbase + j * WAVE;
-            if (idx < n) out[idx] = k[j];
+            for (int j = 0; j < KPT; ++j) {
+                a &= k[j] ^ flip;
+                o |= k[j] ^ flip;
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t idx = wbase + j * WAVE;
+                const bool ok = idx < n;
+                k[j] = ok ? ld_stream<NT_TILE>(in + idx) : sentinel;
+                const uint32_t x = k[j] ^ flip;
+                a &= ok ? x : ~0u;
+                o |= ok ? x : 0u;
+            }
         }
-    }
-    if constexpr (KV) {
+        have_pf = false;
+        // bits on which the tile's keys differ -> passes that are not the identity
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t idx = wbase + j * WAVE;
-            if (idx < n) vout[idx] = v[j];
+        for (int off = 32; off > 0; off >>= 1) {
+            a &= __shfl_xor(a, off);
+            o |= __shfl_xor(o, off);
         }
+        if (lane == 0) {
+            sm.red_and[wid] = a;
+            sm.red_or[wid] = o;
+        }
+        __syncthreads();
+        const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
+        uint32_t diff = 0;
+        {
+            uint32_t aa = ~0u, oo = 0u;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                aa &= sm.red_and[w];
+                oo |= sm.red_or[w];
+            }
+            diff = aa ^ oo;
+        }
+        // next tile of this workgroup (persistent grid), prefetched before the last pass
+        const uint32_t tn = tb + gridDim.x;
+        const bool pf_next = PFK > 0 && tn < n / (uint32_t)TILE;  // the next tile is a full one
+        const int last = diff ? (31 - __builtin_clz(diff)) / 8 : -1;
+        uint32_t *wh = sm.whist + wid * R;
+        for (int pass = 0; pass < 4; ++pass) {
+            const uint32_t shift = pass * 8;
+            if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the block
+            if (PFK > 0 && pf_next && pass == last) {
+                const uint32_t nb = tn * (uint32_t)TILE + wid * (KPT * WAVE) + lane;
+#pragma unroll
+                for (int j = 0; j < PFK; ++j) pf[j] = ld_stream<NT_TILE>(in + nb + j * WAVE);
+                have_pf = true;
+            }
+            for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
+            uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                // stable wave rank: lane-ordered returning atomic, else peers by 8 ballots
+                const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+                uint32_t r;
+                if (atomic_rank) {
+                    r = wave_atomic_rank(wh, d, lane);
+                } else {
+                    const uint64_t m = match8(d);
+                    const uint32_t pre = mbcnt64(m);
+                    const uint32_t old = wh[d];
+                    if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
+                    r = old + pre;
+                }
+                rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
+            }
+            __syncthreads();
+            // tile-wide digit offsets folded into the per-wave offsets: the reorder then
+            // reads one LDS word per key instead of two (LDS was busy 68 % of the kernel,
+            // 60 % of it bank conflicts: profiles/r17_pmc_tile_sort.txt)
+            uint32_t tot = 0;
+            if (tid < (uint32_t)R) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) tot += sm.whist[w * R + tid];
+            }
+            const uint32_t ds = block_excl_scan<BLOCK, R>(tot, sm.wsum);
+            if (tid < (uint32_t)R) {
+                uint32_t run = ds;
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t c = sm.whist[w * R + tid];
+                    sm.whist[w * R + tid] = run;
+                    run += c;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+                const uint32_t dst = wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
+                sm.keys[dst] = k[j];
+                if constexpr (KV) sm.vals[dst] = v[j];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
+            if constexpr (KV) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) v[j] = sm.vals[wid * (KPT * WAVE) + j * WAVE + lane];
+            }
+        }
+        if (full) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t idx = wbase + j * WAVE;
+                if (idx < n) out[idx] = k[j];
+            }
+        }
+        if constexpr (KV) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t idx = wbase + j * WAVE;
+                if (idx < n) vout[idx] = v[j];
+            }
+        }
+        // a uniform tile runs no pass barrier: keep the next tile's red_and/red_or writes
+        // behind every wave's reads of this tile's
+        if (!LABSORT_TS_PERSIST) break;  // one tile per workgroup
+        if (diff == 0u) __syncthreads();
     }
 }
 
@@ -1807,7 +1837,8 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) 
 
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    const unsigned g = (unsigned)((n + TS_TILE - 1) / TS_TILE);
+    const size_t nt = (n + TS_TILE - 1) / TS_TILE;
+    const unsigned g = (unsigned)(LABSORT_TS_PERSIST && nt > (size_t)cu_count() ? (size_t)cu_count() : nt);
     k_tile_sort<TS_BLOCK, TS_KPT><<<g, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
     return hipGetLastError();
 }
