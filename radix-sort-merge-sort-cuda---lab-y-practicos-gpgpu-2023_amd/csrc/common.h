@@ -18,6 +18,12 @@ constexpr int HIST_BLOCK = 1024;
 // ---- persistent pipelined onesweep (8-bit digits) ----
 // The OSP_* shape constants can be overridden (-DLABSORT_OSP_BLOCK=... etc.) for
 // diagnostic builds under harness/exp; the shipped library uses the defaults.
+// r26 A/B at 2^28 (profiles/r26_ab_shapes_tilesort.txt): 768 threads x 20 keys (15360-key
+// tiles, 12 waves, 168 VGPRs: the prefetch without spills, no match buffer) 0.487 / 0.465
+// ms per pass (uniform / sorted keys) vs 0.492 / 0.489 for 1024 x 16, but 0.512 / 0.489
+// with the match-rank buffer in LDS, and its key/value pass 1.00 vs 0.925 ms (11 VGPRs
+// spilled); 768 x 24-32 without the prefetch 0.507-0.513; 512 x 16 at 2 workgroups per
+// CU 0.585.  1024 x 16 is kept: one shape for the key and key/value passes.
 #ifndef LABSORT_OSP_BLOCK
 #define LABSORT_OSP_BLOCK 1024
 #endif

@@ -704,6 +704,9 @@ __device__ __forceinline__ uint32_t osp_load(const uint32_t *p) { return ld_stre
 #define LABSORT_OSP_BUF 1
 #endif
 constexpr bool OSP_BUF = LABSORT_OSP_BUF != 0;
+#ifndef LABSORT_OSP_LBASE
+#define LABSORT_OSP_LBASE 1  // the segments' output bases in LDS (else read from the SegPlan)
+#endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t osp_rsrc(const uint32_t *p, uint32_t n) {
     const uint64_t a = (uint64_t)p;  // wave-uniform: readfirstlane lets the compiler prove it
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
@@ -719,12 +722,12 @@ struct OspSmem {
     uint32_t keys[TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0)];  // padded: see osp_pad
     uint32_t vals[KV ? TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0) : 1];  // key/value: payloads, reordered alike
     uint32_t wh[W * R];
-    uint64_t match[MATCH && !KV && OSP_KPT <= 16 ? W * R : 1];  // (no room beside bigger tiles)
+    uint64_t match[MATCH && !KV && OSP_TILE <= 16384 ? W * R : 1];  // (no room beside bigger tiles)
     uint32_t probe[WAVE];
     uint32_t ordered;
     uint32_t hist[R];
     uint32_t delta[R];
-    uint32_t base[OSP_BUF && !KV ? NSEG * R : 1];  // the segments' output bases (SegPlan::base)
+    uint32_t base[OSP_BUF && !KV && LABSORT_OSP_LBASE ? NSEG * R : 1];  // the segments' output bases (SegPlan::base)
     uint32_t start[NSEG + 1];
     uint32_t tpre[NSEG + 1];
     uint32_t wsum[8];
@@ -767,7 +770,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     // key/value: A's payloads are scattered straight from the LDS reorder buffer (they
     // stay there until B's reorder, after barrier 3), not held in 16 VGPRs
     constexpr bool LDSV = KV && LABSORT_OSP_KV_LDSV;
-    constexpr bool LBASE = OSP_BUF && !KV;    // bases table in LDS
+    constexpr bool LBASE = OSP_BUF && !KV && LABSORT_OSP_LBASE;  // bases table in LDS
     static_assert(!KV || OSP_BUF, "key/value passes use the buffer-descriptor loads and stores");
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW, LBW2 = OSP_LBW2;
     static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
@@ -969,7 +972,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                     const uint32_t r = wave_atomic_rank(wh, d, lane);
                     rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
                 } else {
-                    const uint64_t m = (RANK != OSP_RANK_BALLOT && !KV && OSP_KPT <= 16) ? lds_peers(wm + d, lane)
+                    const uint64_t m = (RANK != OSP_RANK_BALLOT && !KV && OSP_TILE <= 16384) ? lds_peers(wm + d, lane)
                                                                                           : match8(d);
                     const uint32_t pre = mbcnt64(m);
                     const uint32_t old = wh[d];
@@ -1749,7 +1752,7 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
         variant = (e && e[0] >= '0' && e[0] <= '2' && e[1]) ? ((e[0] - '0') << 1) | (e[1] == '1') : OSP_DEFAULT_VARIANT;
     }
     if (vb) {  // key/value: the default variant (lane-ordered atomic rank) only
-        if constexpr (OSP_KPT <= 16) {  // keys + payloads in LDS: 16384-pair tiles at most
+        if constexpr (OSP_TILE <= 16384) {  // keys + payloads in LDS: 16384-pair tiles at most
             k_onesweep_p<2, false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback,
                                                                  counter, err, *vb);
             return hipGetLastError();
