@@ -704,6 +704,15 @@ __device__ __forceinline__ uint32_t osp_load(const uint32_t *p) { return ld_stre
 #define LABSORT_OSP_BUF 1
 #endif
 constexpr bool OSP_BUF = LABSORT_OSP_BUF != 0;
+// LABSORT_OSP_2BAR: two workgroup barriers per tile instead of four.  After barrier (2)
+// every wave reads all waves' digit counts of B (one 16-B LDS read per wave row and lane,
+// 4 digits per lane), scans them itself and writes its own digit offsets, so the
+// aggregate scan's barrier (2b) and the offsets' barrier (3) go; wave 0 publishes B's
+// aggregate.  Keys-only passes with the histogram after the rank (the default variant).
+#ifndef LABSORT_OSP_2BAR
+#define LABSORT_OSP_2BAR 0
+#endif
+constexpr bool OSP_2BAR = LABSORT_OSP_2BAR != 0;
 #ifndef LABSORT_OSP_LBASE
 #define LABSORT_OSP_LBASE 1  // the segments' output bases in LDS (else read from the SegPlan)
 #endif
@@ -728,6 +737,9 @@ struct OspSmem {
     uint32_t hist[R];
     uint32_t delta[R];
     uint32_t base[OSP_BUF && !KV && LABSORT_OSP_LBASE ? NSEG * R : 1];  // the segments' output bases (SegPlan::base)
+    uint32_t woff[OSP_2BAR && !KV ? W * R : 1];  // two-barrier loop: each wave's digit offsets
+    uint32_t agg[OSP_2BAR && !KV ? R : 1];       // two-barrier loop: B's tile histogram and digit
+    uint32_t dst0[OSP_2BAR && !KV ? R : 1];      //   starts, handed to the digit threads
     uint32_t start[NSEG + 1];
     uint32_t tpre[NSEG + 1];
     uint32_t wsum[8];
@@ -771,6 +783,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     // stay there until B's reorder, after barrier 3), not held in 16 VGPRs
     constexpr bool LDSV = KV && LABSORT_OSP_KV_LDSV;
     constexpr bool LBASE = OSP_BUF && !KV && LABSORT_OSP_LBASE;  // bases table in LDS
+    constexpr bool TWO_BAR = OSP_2BAR && !KV && !HIST_FIRST;
     static_assert(!KV || OSP_BUF, "key/value passes use the buffer-descriptor loads and stores");
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW, LBW2 = OSP_LBW2;
     static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
@@ -1039,7 +1052,47 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         OSP_T(2, 3);  // look-back completion of A (waves 0-3)
         __syncthreads();  // (2) delta of A, wave counts and wsum of B
         OSP_T(3, 0);
-        if (!HIST_FIRST && haveB) {
+        if (TWO_BAR && haveB) {
+            // every wave: B's histogram for digits 4 lane .. 4 lane + 3 and the counts of the
+            // waves before it, from all waves' counters; its own digit offsets from a wave scan
+            uint32_t t4[4] = {0u, 0u, 0u, 0u}, p4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint4 c = *reinterpret_cast<const uint4 *>(sm.wh + w * R + 4u * lane);
+                t4[0] += c.x;
+                t4[1] += c.y;
+                t4[2] += c.z;
+                t4[3] += c.w;
+                if ((uint32_t)w < wid) {
+                    p4[0] += c.x;
+                    p4[1] += c.y;
+                    p4[2] += c.z;
+                    p4[3] += c.w;
+                }
+            }
+            if (lane == 63u) t4[3] -= (uint32_t)TILE - nvalidB;  // digit 255: the sentinels (last in the tile)
+            const uint32_t s4 = t4[0] + t4[1] + t4[2] + t4[3];
+            uint32_t x = s4;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (lane >= (uint32_t)off) x += y;
+            }
+            uint32_t d4[4];
+            d4[0] = x - s4;
+            d4[1] = d4[0] + t4[0];
+            d4[2] = d4[1] + t4[1];
+            d4[3] = d4[2] + t4[2];
+            *reinterpret_cast<uint4 *>(sm.woff + wid * R + 4u * lane) =
+                uint4{d4[0] + p4[0], d4[1] + p4[1], d4[2] + p4[2], d4[3] + p4[3]};
+            if (wid == 0) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    st_agent(lookback + (size_t)slotB * R + 4u * lane + q, (lB == 0 ? LB_INC : LB_AGG) | t4[q]);
+                *reinterpret_cast<uint4 *>(sm.agg + 4u * lane) = uint4{t4[0], t4[1], t4[2], t4[3]};
+                *reinterpret_cast<uint4 *>(sm.dst0 + 4u * lane) = uint4{d4[0], d4[1], d4[2], d4[3]};
+            }
+        } else if (!HIST_FIRST && haveB) {
             // tile histogram = sum of the per-wave counts; publish B's aggregate, scan it
             if (tid < (uint32_t)R) {
                 uint32_t tot = 0;
@@ -1087,9 +1140,9 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         }
         OSP_T(4, 0);  // aggregate of B, scatter of A issued
         if (!haveB) break;
-        if constexpr (!HIST_FIRST) __syncthreads();  // (2b) wsum of B
+        if constexpr (!HIST_FIRST && !TWO_BAR) __syncthreads();  // (2b) wsum of B
         OSP_T(5, 0);
-        if (tid < (uint32_t)R) {
+        if (!TWO_BAR && tid < (uint32_t)R) {
             uint32_t add = 0;
 #pragma unroll
             for (int w = 0; w < 4; ++w)
@@ -1107,11 +1160,12 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         }
         if (tid == 0) sm.next = (!PF || cC != OSP_DONE) ? acquire() : OSP_DONE;
         OSP_T(6, 0);  // wave offsets (waves 0-3), acquisition
-        __syncthreads();  // (3) wave offsets of B
+        if constexpr (!TWO_BAR) __syncthreads();  // (3) wave offsets of B
         OSP_T(7, 0);
+        const uint32_t *wo = TWO_BAR ? sm.woff + wid * R : wh;
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            const uint32_t pos = osp_pad(wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu));
+            const uint32_t pos = osp_pad(wo[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu));
             sm.keys[pos] = kB[j];
             if constexpr (KV) sm.vals[pos] = vB[j];
         }
@@ -1133,6 +1187,12 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         segA = segB;
         nvalidA = nvalidB;
         aggA = hB;
+        if constexpr (TWO_BAR) {  // B's histogram and digit starts, from wave 0 (before barrier 4)
+            if (tid < (uint32_t)R) {
+                aggA = sm.agg[tid];
+                dstartA = sm.dst0[tid];
+            }
+        }
         if constexpr (PF) {
             cB = cC;
             cC = sm.next;
