@@ -1052,7 +1052,9 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         OSP_T(2, 3);  // look-back completion of A (waves 0-3)
         __syncthreads();  // (2) delta of A, wave counts and wsum of B
         OSP_T(3, 0);
-        if (TWO_BAR && haveB) {
+        // two-barrier loop: wave 0 scans B first (it publishes B's aggregate), the other
+        // waves after issuing A's scatter (the stores are the pass's bound: issue them first)
+        auto b_offsets = [&]() {
             // every wave: B's histogram for digits 4 lane .. 4 lane + 3 and the counts of the
             // waves before it, from all waves' counters; its own digit offsets from a wave scan
             uint32_t t4[4] = {0u, 0u, 0u, 0u}, p4[4] = {0u, 0u, 0u, 0u};
@@ -1092,7 +1094,9 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                 *reinterpret_cast<uint4 *>(sm.agg + 4u * lane) = uint4{t4[0], t4[1], t4[2], t4[3]};
                 *reinterpret_cast<uint4 *>(sm.dst0 + 4u * lane) = uint4{d4[0], d4[1], d4[2], d4[3]};
             }
-        } else if (!HIST_FIRST && haveB) {
+        };
+        if (TWO_BAR && haveB && wid == 0) b_offsets();
+        if (!TWO_BAR && !HIST_FIRST && haveB) {
             // tile histogram = sum of the per-wave counts; publish B's aggregate, scan it
             if (tid < (uint32_t)R) {
                 uint32_t tot = 0;
@@ -1138,6 +1142,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
                 }
             }
         }
+        if (TWO_BAR && haveB && wid != 0) b_offsets();
         OSP_T(4, 0);  // aggregate of B, scatter of A issued
         if (!haveB) break;
         if constexpr (!HIST_FIRST && !TWO_BAR) __syncthreads();  // (2b) wsum of B
