@@ -7,6 +7,7 @@ R="$(cd "$(dirname "$0")/../.." && pwd)"
 C="$R/radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd/csrc"
 B="$(mktemp -d)"
 F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 ${STAMPS--DOSP_STAMPS} ${EXTRA_FLAGS:-}"
-for f in kernels kmerge gsweep api multi thrust_host; do /opt/rocm/bin/hipcc $F -c "$C/$f.hip" -o "$B/$f.o" & done; wait
+SRCS=$(sed -n "s/^SRCS := //p" "$C/Makefile" | sed "s/\.hip//g")  # the product sources
+for f in $SRCS; do /opt/rocm/bin/hipcc $F -c "$C/$f.hip" -o "$B/$f.o" & done; wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$R/harness/exp/liblabsort_stamps${SUFFIX:-}.so" "$B"/*.o -ldl -lpthread
 rm -rf "$B"

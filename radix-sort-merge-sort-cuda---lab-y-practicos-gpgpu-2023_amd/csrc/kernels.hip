@@ -219,6 +219,9 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) atomicAdd(&h[(k[j] & 255u) * SL + slot], 1u);
+#ifdef LABSORT_HS_DIAG_NOJOINT
+        return;  // diagnostic timing build: digit 0 only (results invalid)
+#endif
         if (__ballot(fld(k[0], 2) == fld(k[3], 2)) == 0ull) {  // no repeats here
 #pragma unroll
             for (int p = 0; p < 3; ++p)
@@ -713,6 +716,10 @@ constexpr bool OSP_BUF = LABSORT_OSP_BUF != 0;
 #define LABSORT_OSP_2BAR 0
 #endif
 constexpr bool OSP_2BAR = LABSORT_OSP_2BAR != 0;
+#ifndef LABSORT_OSP_EARLY_ACQ
+#define LABSORT_OSP_EARLY_ACQ 1  // r26: 0.4906 -> 0.4729 ms per pass at 2^28 (barrier 3: 11.9 -> 7.1 % of wave time)
+#endif
+constexpr bool OSP_EARLY_ACQ = LABSORT_OSP_EARLY_ACQ != 0;
 #ifndef LABSORT_OSP_LBASE
 #define LABSORT_OSP_LBASE 1  // the segments' output bases in LDS (else read from the SegPlan)
 #endif
@@ -835,6 +842,23 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         }
         return OSP_DONE;
     };
+    // LABSORT_OSP_EARLY_ACQ: the in-loop acquisition's counter increment is issued by tid 0
+    // at the top of the iteration and its result consumed before barrier (3), so the
+    // atomic's round trip overlaps the iteration instead of holding every wave at the
+    // barrier; the segment's tile count comes from LDS
+    auto acquire_done = [&](uint32_t c) {  // c: atomicAdd(counter + group gk), issued earlier
+        while (gk < G) {
+            const uint32_t grp = (home + gk) & (G - 1u);
+            if (c >= climit) {
+                if (++gk < G) c = atomicAdd(counter + ((home + gk) & (G - 1u)), 1u);
+                continue;
+            }
+            const uint32_t sg = grp | ((c & lmask) << gbits), l = c >> lbits;
+            if (l < sm.tpre[sg + 1] - sm.tpre[sg]) return l * NSEG + sg;
+            c = atomicAdd(counter + grp, 1u);
+        }
+        return OSP_DONE;
+    };
     if (tid == 0) {
         const uint32_t c0 = acquire();
         sm.next = c0;
@@ -936,6 +960,9 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             for (int j = 0; j < KPT; ++j) kB[j] = kN[j < (PF ? KPT : 1) ? j : 0];
         }
         const bool haveB = cB != OSP_DONE;
+        uint32_t acq_c = 0;  // tid 0: the early counter increment (EARLY_ACQ)
+        if (OSP_EARLY_ACQ && tid == 0 && (!PF || cC != OSP_DONE) && gk < G)
+            acq_c = atomicAdd(counter + ((home + gk) & (G - 1u)), 1u);
         const uint32_t segB = cB & segmask, lB = cB >> segbits;
         const uint32_t loB = haveB ? sm.tpre[segB] : 0u, slotB = loB + lB;
         uint32_t begB = 0, nvalidB = 0;
@@ -1163,7 +1190,8 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             sm.hist[tid] = 0u;
             dstartA = ds;
         }
-        if (tid == 0) sm.next = (!PF || cC != OSP_DONE) ? acquire() : OSP_DONE;
+        if (tid == 0)
+            sm.next = (!PF || cC != OSP_DONE) ? (OSP_EARLY_ACQ ? acquire_done(acq_c) : acquire()) : OSP_DONE;
         OSP_T(6, 0);  // wave offsets (waves 0-3), acquisition
         if constexpr (!TWO_BAR) __syncthreads();  // (3) wave offsets of B
         OSP_T(7, 0);
