@@ -791,6 +791,9 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     constexpr bool LDSV = KV && LABSORT_OSP_KV_LDSV;
     constexpr bool LBASE = OSP_BUF && !KV && LABSORT_OSP_LBASE;  // bases table in LDS
     constexpr bool TWO_BAR = OSP_2BAR && !KV && !HIST_FIRST;
+    // early acquisition with the prefetch only: the key/value pass (no prefetch) measured
+    // 0.978 vs 0.932 ms per pass with it (profiles/r26_ab_early_acquire.txt)
+    constexpr bool EACQ = OSP_EARLY_ACQ && PF;
     static_assert(!KV || OSP_BUF, "key/value passes use the buffer-descriptor loads and stores");
     constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW, LBW2 = OSP_LBW2;
     static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
@@ -961,7 +964,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         }
         const bool haveB = cB != OSP_DONE;
         uint32_t acq_c = 0;  // tid 0: the early counter increment (EARLY_ACQ)
-        if (OSP_EARLY_ACQ && tid == 0 && (!PF || cC != OSP_DONE) && gk < G)
+        if (EACQ && tid == 0 && (!PF || cC != OSP_DONE) && gk < G)
             acq_c = atomicAdd(counter + ((home + gk) & (G - 1u)), 1u);
         const uint32_t segB = cB & segmask, lB = cB >> segbits;
         const uint32_t loB = haveB ? sm.tpre[segB] : 0u, slotB = loB + lB;
@@ -1191,7 +1194,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             dstartA = ds;
         }
         if (tid == 0)
-            sm.next = (!PF || cC != OSP_DONE) ? (OSP_EARLY_ACQ ? acquire_done(acq_c) : acquire()) : OSP_DONE;
+            sm.next = (!PF || cC != OSP_DONE) ? (EACQ ? acquire_done(acq_c) : acquire()) : OSP_DONE;
         OSP_T(6, 0);  // wave offsets (waves 0-3), acquisition
         if constexpr (!TWO_BAR) __syncthreads();  // (3) wave offsets of B
         OSP_T(7, 0);
