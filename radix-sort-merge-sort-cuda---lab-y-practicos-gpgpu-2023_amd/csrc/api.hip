@@ -214,7 +214,6 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
         HIP_TRY(launch_zero(ws + L.off_lookback, L.zero_bytes - L.off_lookback, s));
         HIP_TRY(launch_plan8(hps, joint, n, in == out ? 1 : 0, plan, sps, hist, s));
         for (int p = 0; p < L.P; ++p) {
-            if (p > 0) HIP_TRY(launch_segplan(plan, p, n, hist, joint, sps, s));
             TimingScope ts(LABSORT_K_ONESWEEP, s);
             HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
                                       counters + (size_t)p * OSP_NCTR, err, s));
@@ -232,7 +231,9 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
                                     counters + (size_t)p * OSP_NCTR, err, s));
         }
     }
-    HIP_TRY(launch_final_copy(b, plan, n, s));
+    // 8-bit: pass 0's launch copies an input whose every digit is constant (IN -> OUT), so
+    // only an in-place sort (its odd pass count ends in TMP) needs the final copy launch
+    if (bits != 8 || in == out) HIP_TRY(launch_final_copy(b, plan, n, s));
     return LABSORT_OK;
 }
 
@@ -780,7 +781,6 @@ int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint3
         HIP_TRY(launch_zero(ws + L.off_lookback, L.zero_bytes - L.off_lookback, s));
         HIP_TRY(launch_plan8(hps, joint, n, ki == ko ? 1 : 0, plan, sps, hist, s));
         for (int p = 0; p < L.P; ++p) {
-            if (p > 0) HIP_TRY(launch_segplan(plan, p, n, hist, joint, sps, s));
             TimingScope ts(LABSORT_K_ONESWEEP, s);
             HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
                                       counters + (size_t)p * OSP_NCTR, err, s, &vb));
@@ -798,8 +798,10 @@ int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint3
                                     counters + (size_t)p * OSP_NCTR, err, s, &vb));
         }
     }
-    HIP_TRY(launch_final_copy(b, plan, n, s));
-    HIP_TRY(launch_final_copy(vb, plan, n, s));
+    if (!pairs_persistent() || ki == ko) {  // (persistent: as sort_radix)
+        HIP_TRY(launch_final_copy(b, plan, n, s));
+        HIP_TRY(launch_final_copy(vb, plan, n, s));
+    }
     return LABSORT_OK;
 }
 }  // namespace

@@ -276,8 +276,6 @@ hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32
                            hipStream_t s);
 hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, int in_is_out, Plan *plan,
                         SegPlan *segplans, uint32_t *hist, hipStream_t s);
-hipError_t launch_segplan(const Plan *plan, int pass, size_t n, const uint32_t *hist, const uint32_t *joint,
-                          SegPlan *segplans, hipStream_t s);
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
                              uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s,
                              const Bufs *vb = nullptr);

@@ -364,8 +364,43 @@ __device__ void build_segplan(SegPlan *__restrict__ sp, const uint32_t *__restri
     }
 }
 
+// SegPlan of pass q when q is active and not the first: segments = ranges of the
+// previous digit's top nibble (starts from its histogram), histograms = the joint
+// counts k_hist_seg wrote; one chain when the previous active digit is not q - 1.
+// 256 threads; hist: the 4 digit histograms; sh, start: LDS scratch.
+__device__ void build_segplan_later(SegPlan *__restrict__ sps, int q, uint32_t prev, uint32_t n, int seg_later,
+                                    const uint32_t *hist, const uint32_t *__restrict__ joint, uint32_t *sh,
+                                    uint32_t *start) {
+    const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
+    if (seg_later <= 0 || prev + 1u != (uint32_t)q) {  // one chain over the whole input
+        for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[q * 256 + t];
+        if (t <= (uint32_t)NSEG) start[t] = t ? n : 0u;
+        __syncthreads();
+        build_segplan(sps + q, sh, start, 2u, sh);
+        return;
+    }
+    // segment starts: exclusive prefix over nibble groups of hist[prev]
+    const uint32_t v = hist[prev * 256 + t];
+    uint32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    if (lane == 63) sh[NSEG * 256 + wid] = x;
+    __syncthreads();
+    uint32_t add = 0;
+    for (uint32_t w = 0; w < wid; ++w) add += sh[NSEG * 256 + w];
+    if ((t & 15u) == 0) start[t >> 4] = x + add - v;
+    if (t == 0) start[NSEG] = n;
+    __syncthreads();
+    build_segplan(sps + q, joint + (size_t)q * NSEG * 256, start, 1u, sh);
+}
+
 // Pass plan for the 8-bit radix (as k_plan: totals, trivial passes, ping-pong
-// buffers; plus each pass's next active digit) and the first active pass's SegPlan.
+// buffers; plus each pass's next active digit) and every active pass's SegPlan (the
+// later passes' plans depend only on the histograms, so they are built here, not by
+// a launch before each pass).
 __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps, const uint32_t *__restrict__ joint,
                                                uint32_t n, int in_is_out, int seg_later, Plan *__restrict__ plan,
                                                SegPlan *__restrict__ sps, uint32_t *__restrict__ hist_out) {
@@ -373,6 +408,7 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
     __shared__ uint32_t sh[NSEG * 256 + 8];
     __shared__ uint32_t triv[4];
     __shared__ uint32_t start[NSEG + 1];
+    __shared__ uint32_t prevs[4];
     __shared__ int first;
     const uint32_t t = threadIdx.x;
     if (t < 4) triv[t] = 0;
@@ -400,9 +436,14 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
             plan->next[p] = NEXT_NONE;
             plan->prev[p] = NEXT_NONE;
         }
-        for (int p = 0; p < 4; ++p)
+        for (int p = 0; p < 4; ++p) {
+            prevs[p] = NEXT_NONE;
             if (!triv[p]) act[k++] = p;
-        for (int i = 0; i + 1 < k; ++i) plan->next[act[i]] = (uint32_t)act[i + 1];
+        }
+        for (int i = 0; i + 1 < k; ++i) {
+            plan->next[act[i]] = (uint32_t)act[i + 1];
+            prevs[act[i + 1]] = (uint32_t)act[i];
+        }
         plan->active = (uint32_t)k;
         first = k ? act[0] : -1;
         if (k == 0) {
@@ -434,47 +475,17 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
         for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[first * 256 + t];
         __syncthreads();
         build_segplan(sps + first, sh, start, 2u, sh);
-        return;
-    }
-    for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = hps[s * 256 + t];
-    __syncthreads();
-    build_segplan(sps + first, sh, start, 0u, sh);
-}
-
-// SegPlan of pass q when q is active and not the first: segments = ranges of the
-// previous digit's top nibble (starts from its histogram), histograms = the joint
-// counts k_hist_seg wrote; one chain when the previous active digit is not q - 1.
-__global__ __launch_bounds__(256) void k_segplan(const Plan *__restrict__ plan, int q, uint32_t n, int seg_later,
-                                                 const uint32_t *__restrict__ hist, const uint32_t *__restrict__ joint,
-                                                 SegPlan *__restrict__ sps) {
-    __shared__ uint32_t sh[NSEG * 256 + 8];
-    __shared__ uint32_t start[NSEG + 1];
-    const uint32_t prev = plan->prev[q];
-    if (plan->src[q] == SEL_SKIP || prev == NEXT_NONE) return;
-    const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
-    if (seg_later <= 0 || prev + 1u != (uint32_t)q) {  // one chain over the whole input
-        for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[q * 256 + t];
-        if (t <= (uint32_t)NSEG) start[t] = t ? n : 0u;
+    } else {
+        for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = hps[s * 256 + t];
         __syncthreads();
-        build_segplan(sps + q, sh, start, 2u, sh);
-        return;
+        build_segplan(sps + first, sh, start, 0u, sh);
     }
-    // segment starts: exclusive prefix over nibble groups of hist[prev]
-    const uint32_t v = hist[prev * 256 + t];
-    uint32_t x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= (uint32_t)off) x += y;
+    // the later active passes
+    for (int q = first + 1; q < 4; ++q) {
+        if (prevs[q] == NEXT_NONE) continue;  // (block-uniform)
+        __syncthreads();  // sh, start reused
+        build_segplan_later(sps, q, prevs[q], n, seg_later, hist, joint, sh, start);
     }
-    if (lane == 63) sh[NSEG * 256 + wid] = x;
-    __syncthreads();
-    uint32_t add = 0;
-    for (uint32_t w = 0; w < wid; ++w) add += sh[NSEG * 256 + w];
-    if ((t & 15u) == 0) start[t >> 4] = x + add - v;
-    if (t == 0) start[NSEG] = n;
-    __syncthreads();
-    build_segplan(sps + q, joint + (size_t)q * NSEG * 256, start, 1u, sh);
 }
 
 __global__ __launch_bounds__(256) void k_final_copy(Bufs b, const Plan *__restrict__ plan, size_t n) {
@@ -800,7 +811,26 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     __shared__ S sm;
 
     const uint32_t srcsel = plan->src[pass];
-    if (srcsel == SEL_SKIP) return;  // every key has the same digit: identity pass
+    if (srcsel == SEL_SKIP) {  // every key has the same digit: identity pass
+        if (pass == 0 && plan->copy_from == SEL_IN) {
+            // no active pass at all (every digit constant): the input is the result, and
+            // pass 0's launch copies it (api.hip launches no final copy for in != out)
+            const uint4 *src = reinterpret_cast<const uint4 *>(bufs.p[SEL_IN]);
+            uint4 *dst = reinterpret_cast<uint4 *>(bufs.p[SEL_OUT]);
+            const uint32_t *vsrc = KV ? vbufs.p[SEL_IN] : nullptr;
+            uint32_t *vdst = KV ? vbufs.p[SEL_OUT] : nullptr;
+            const size_t stride = (size_t)gridDim.x * OSP_BLOCK, g0 = (size_t)blockIdx.x * OSP_BLOCK + threadIdx.x;
+            if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
+                for (size_t i = g0; i < n / 4; i += stride) dst[i] = src[i];
+                for (size_t i = (n / 4) * 4 + g0; i < n; i += stride) bufs.p[SEL_OUT][i] = bufs.p[SEL_IN][i];
+            } else {
+                for (size_t i = g0; i < n; i += stride) bufs.p[SEL_OUT][i] = bufs.p[SEL_IN][i];
+            }
+            if constexpr (KV)
+                for (size_t i = g0; i < n; i += stride) vdst[i] = vsrc[i];
+        }
+        return;
+    }
     const uint32_t *__restrict__ in = bufs.p[srcsel];
     uint32_t *__restrict__ out = bufs.p[plan->dst[pass]];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
@@ -1904,11 +1934,6 @@ hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, in
     return hipGetLastError();
 }
 
-hipError_t launch_segplan(const Plan *plan, int pass, size_t n, const uint32_t *hist, const uint32_t *joint,
-                          SegPlan *segplans, hipStream_t s) {
-    k_segplan<<<1, 256, 0, s>>>(plan, pass, (uint32_t)n, seg_later(), hist, joint, segplans);
-    return hipGetLastError();
-}
 
 // Zero a workspace range with a kernel instead of hipMemsetAsync: the sorts' zeroing must
 // replay inside captured HIP graphs (tests/test_gpu_graph.py), which a kernel node does.

@@ -104,11 +104,17 @@ def test_sort_device_uniform(ls, oracle, torch_gpu, algo, key, n):
     np.testing.assert_array_equal(from_dev(t), a)  # input untouched
 
 
-@pytest.mark.parametrize("algo", ["radix", "merge"])
+@pytest.mark.parametrize("algo", ["radix", "merge", "radix-onesweep"])
 @pytest.mark.parametrize("dist", DISTS)
 @pytest.mark.parametrize("inplace", [False, True])
-def test_sort_device_distributions(ls, oracle, torch_gpu, algo, dist, inplace):
+def test_sort_device_distributions(ls, oracle, torch_gpu, monkeypatch, algo, dist, inplace):
+    """radix-onesweep: the onesweep passes at this size (LABSORT_RADIX_IMPL=onesweep): a
+    constant input (no active pass: pass 0's launch copies it; in place: nothing to do),
+    one or two active passes in place (the final copy) and the segmented plans."""
     torch = torch_gpu
+    if algo == "radix-onesweep":
+        monkeypatch.setenv("LABSORT_RADIX_IMPL", "onesweep")
+        algo = "radix"
     n = 300_007
     a = oracle.gen(n, SEED + 6, dist, param=(0xABCDEF if dist == "const" else 11))
     for key in ("u32", "i32"):
@@ -353,8 +359,11 @@ def test_timing_hooks(ls, oracle, torch_gpu, monkeypatch, impl):
 ])
 @pytest.mark.parametrize("key", ["u32", "i32"])
 @pytest.mark.parametrize("n", [8192 * 16 + 5, (1 << 21) + 777])
-def test_sort_device_pass_structure(ls, oracle, torch_gpu, mask, name, key, n):
+@pytest.mark.parametrize("impl", ["", "onesweep"])
+def test_sort_device_pass_structure(ls, oracle, torch_gpu, monkeypatch, mask, name, key, n, impl):
     torch = torch_gpu
+    if impl:
+        monkeypatch.setenv("LABSORT_RADIX_IMPL", impl)
     a = oracle.gen(n, SEED + 16, "u32") & np.uint32(mask)
     t = to_dev(torch, a)
     o = torch.empty_like(t)
