@@ -727,6 +727,15 @@ constexpr bool OSP_BUF = LABSORT_OSP_BUF != 0;
 #define LABSORT_OSP_2BAR 0
 #endif
 constexpr bool OSP_2BAR = LABSORT_OSP_2BAR != 0;
+// LABSORT_OSP_W0SCAN: wave 0 alone sums B's 16 wave counts (4 digits per lane, 16-B LDS
+// reads), scans them with one wave scan, publishes B's aggregate and writes every wave's
+// digit offsets, while the other waves issue A's scatter: no cross-wave scan, so the
+// aggregate's barrier (2b) goes (three barriers per tile).  Keys-only passes with the
+// histogram after the rank (the default variant).
+#ifndef LABSORT_OSP_W0SCAN
+#define LABSORT_OSP_W0SCAN 0
+#endif
+constexpr bool OSP_W0SCAN = LABSORT_OSP_W0SCAN != 0;
 #ifndef LABSORT_OSP_EARLY_ACQ
 #define LABSORT_OSP_EARLY_ACQ 1  // r26: 0.4906 -> 0.4729 ms per pass at 2^28 (barrier 3: 11.9 -> 7.1 % of wave time)
 #endif
@@ -756,8 +765,8 @@ struct OspSmem {
     uint32_t delta[R];
     uint32_t base[OSP_BUF && !KV && LABSORT_OSP_LBASE ? NSEG * R : 1];  // the segments' output bases (SegPlan::base)
     uint32_t woff[OSP_2BAR && !KV ? W * R : 1];  // two-barrier loop: each wave's digit offsets
-    uint32_t agg[OSP_2BAR && !KV ? R : 1];       // two-barrier loop: B's tile histogram and digit
-    uint32_t dst0[OSP_2BAR && !KV ? R : 1];      //   starts, handed to the digit threads
+    uint32_t agg[(OSP_2BAR || OSP_W0SCAN) && !KV ? R : 1];   // two-barrier / wave-0 scan: B's tile
+    uint32_t dst0[(OSP_2BAR || OSP_W0SCAN) && !KV ? R : 1];  //   histogram and digit starts
     uint32_t start[NSEG + 1];
     uint32_t tpre[NSEG + 1];
     uint32_t wsum[8];
@@ -802,6 +811,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     constexpr bool LDSV = KV && LABSORT_OSP_KV_LDSV;
     constexpr bool LBASE = OSP_BUF && !KV && LABSORT_OSP_LBASE;  // bases table in LDS
     constexpr bool TWO_BAR = OSP_2BAR && !KV && !HIST_FIRST;
+    constexpr bool W0 = OSP_W0SCAN && !TWO_BAR && !KV && !HIST_FIRST;
     // early acquisition with the prefetch only: the key/value pass (no prefetch) measured
     // 0.978 vs 0.932 ms per pass with it (profiles/r26_ab_early_acquire.txt)
     constexpr bool EACQ = OSP_EARLY_ACQ && PF;
@@ -1156,7 +1166,50 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             }
         };
         if (TWO_BAR && haveB && wid == 0) b_offsets();
-        if (!TWO_BAR && !HIST_FIRST && haveB) {
+        if (W0 && haveB && wid == 0) {
+            // wave 0: B's histogram (4 digits per lane), digit starts, aggregate, and every
+            // wave's digit offsets written over its counts
+            uint32_t t4[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                const uint4 c = *reinterpret_cast<const uint4 *>(sm.wh + w * R + 4u * lane);
+                t4[0] += c.x;
+                t4[1] += c.y;
+                t4[2] += c.z;
+                t4[3] += c.w;
+            }
+            const uint32_t sent = lane == 63u ? (uint32_t)TILE - nvalidB : 0u;  // digit 255: the sentinels
+            const uint32_t s4 = t4[0] + t4[1] + t4[2] + t4[3] - sent;
+            uint32_t x = s4;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (lane >= (uint32_t)off) x += y;
+            }
+            uint32_t d4[4];
+            d4[0] = x - s4;
+            d4[1] = d4[0] + t4[0];
+            d4[2] = d4[1] + t4[1];
+            d4[3] = d4[2] + t4[2];
+            t4[3] -= sent;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                st_agent(lookback + (size_t)slotB * R + 4u * lane + q, (lB == 0 ? LB_INC : LB_AGG) | t4[q]);
+            *reinterpret_cast<uint4 *>(sm.agg + 4u * lane) = uint4{t4[0], t4[1], t4[2], t4[3]};
+            *reinterpret_cast<uint4 *>(sm.dst0 + 4u * lane) = uint4{d4[0], d4[1], d4[2], d4[3]};
+            uint4 r = uint4{d4[0], d4[1], d4[2], d4[3]};
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                uint4 *p = reinterpret_cast<uint4 *>(sm.wh + w * R + 4u * lane);
+                const uint4 c = *p;
+                *p = r;
+                r.x += c.x;
+                r.y += c.y;
+                r.z += c.z;
+                r.w += c.w;
+            }
+        }
+        if (!W0 && !TWO_BAR && !HIST_FIRST && haveB) {
             // tile histogram = sum of the per-wave counts; publish B's aggregate, scan it
             if (tid < (uint32_t)R) {
                 uint32_t tot = 0;
@@ -1205,9 +1258,9 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         if (TWO_BAR && haveB && wid != 0) b_offsets();
         OSP_T(4, 0);  // aggregate of B, scatter of A issued
         if (!haveB) break;
-        if constexpr (!HIST_FIRST && !TWO_BAR) __syncthreads();  // (2b) wsum of B
+        if constexpr (!HIST_FIRST && !TWO_BAR && !W0) __syncthreads();  // (2b) wsum of B
         OSP_T(5, 0);
-        if (!TWO_BAR && tid < (uint32_t)R) {
+        if (!TWO_BAR && !W0 && tid < (uint32_t)R) {
             uint32_t add = 0;
 #pragma unroll
             for (int w = 0; w < 4; ++w)
@@ -1253,7 +1306,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         segA = segB;
         nvalidA = nvalidB;
         aggA = hB;
-        if constexpr (TWO_BAR) {  // B's histogram and digit starts, from wave 0 (before barrier 4)
+        if constexpr (TWO_BAR || W0) {  // B's histogram and digit starts, from wave 0 (before barrier 4)
             if (tid < (uint32_t)R) {
                 aggA = sm.agg[tid];
                 dstartA = sm.dst0[tid];
