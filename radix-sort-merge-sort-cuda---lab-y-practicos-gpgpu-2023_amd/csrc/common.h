@@ -58,6 +58,11 @@ constexpr int NT_OSP = 1, NT_HIST = 2, NT_TILE = 4, NT_MERGE = 8, NT_GS = 16, NT
 constexpr int OSP_BLOCK = LABSORT_OSP_BLOCK;
 constexpr int OSP_KPT = LABSORT_OSP_KPT;
 constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 16384 keys per tile
+// key/value pass threads (the same tile: OSP_TILE / OSP_KV_BLOCK pairs per thread)
+#ifndef LABSORT_OSP_KV_BLOCK
+#define LABSORT_OSP_KV_BLOCK 512  // r26: 0.902 vs 0.939 ms per pair pass (1024 x 16); with the prefetch 1.020
+#endif
+constexpr int OSP_KV_BLOCK = LABSORT_OSP_KV_BLOCK;
 constexpr int OSP_LBW = LABSORT_OSP_LBW;    // look-back window of the first round (predecessor tiles)
 constexpr int OSP_LBW2 = LABSORT_OSP_LBW2;  // look-back window of the later rounds
 constexpr bool OSP_PREFETCH = LABSORT_OSP_PREFETCH != 0;  // next tile's keys loaded one iteration ahead

@@ -754,7 +754,8 @@ constexpr int OSP_BUF_NT = (LABSORT_NT_LOADS & NT_OSP) ? 2 : 0;  // aux bit 1 = 
 
 template <bool MATCH, bool KV = false>
 struct OspSmem {
-    static constexpr int R = 256, W = OSP_BLOCK / WAVE, TILE = OSP_TILE;
+    static constexpr int BLOCK = KV ? OSP_KV_BLOCK : OSP_BLOCK;  // threads (key/value: its own shape)
+    static constexpr int R = 256, W = BLOCK / WAVE, TILE = OSP_TILE;
     uint32_t keys[TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0)];  // padded: see osp_pad
     uint32_t vals[KV ? TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0) : 1];  // key/value: payloads, reordered alike
     uint32_t wh[W * R];
@@ -792,7 +793,8 @@ constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 // (the rank falls back to 8 ballots if the lane-order check fails) nor for the bases
 // table, and the registers none for the next tile's prefetch.
 template <int RANK, bool HIST_FIRST, bool KV = false>
-__global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
+__global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
+                             OSP_BLOCKS_PER_CU *(KV ? OSP_KV_BLOCK : OSP_BLOCK) / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
                                                           uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
                                                           uint32_t *lookback, uint32_t *counter, uint32_t *err,
                                                           Bufs vbufs) {
@@ -814,10 +816,13 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     constexpr bool W0 = OSP_W0SCAN && !TWO_BAR && !KV && !HIST_FIRST;
     // early acquisition with the prefetch only: the key/value pass (no prefetch) measured
     // 0.978 vs 0.932 ms per pass with it (profiles/r26_ab_early_acquire.txt)
-    constexpr bool EACQ = OSP_EARLY_ACQ && PF;
+#ifndef LABSORT_OSP_KV_EACQ
+#define LABSORT_OSP_KV_EACQ 0
+#endif
+    constexpr bool EACQ = OSP_EARLY_ACQ && (PF || (KV && LABSORT_OSP_KV_EACQ));
     static_assert(!KV || OSP_BUF, "key/value passes use the buffer-descriptor loads and stores");
-    constexpr int R = S::R, W = S::W, TILE = S::TILE, KPT = OSP_KPT, LBW = OSP_LBW, LBW2 = OSP_LBW2;
-    static_assert(OSP_BLOCK >= 512 && R <= OSP_BLOCK && NSEG == 16, "digit threads = waves 0-3; c & 15 = segment");
+    constexpr int R = S::R, W = S::W, TILE = S::TILE, BLK = S::BLOCK, KPT = TILE / BLK, LBW = OSP_LBW, LBW2 = OSP_LBW2;
+    static_assert(BLK >= 512 && R <= BLK && NSEG == 16 && KPT * BLK == TILE, "digit threads = waves 0-3; c & 15 = segment");
     __shared__ S sm;
 
     const uint32_t srcsel = plan->src[pass];
@@ -829,7 +834,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             uint4 *dst = reinterpret_cast<uint4 *>(bufs.p[SEL_OUT]);
             const uint32_t *vsrc = KV ? vbufs.p[SEL_IN] : nullptr;
             uint32_t *vdst = KV ? vbufs.p[SEL_OUT] : nullptr;
-            const size_t stride = (size_t)gridDim.x * OSP_BLOCK, g0 = (size_t)blockIdx.x * OSP_BLOCK + threadIdx.x;
+            const size_t stride = (size_t)gridDim.x * BLK, g0 = (size_t)blockIdx.x * BLK + threadIdx.x;
             if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
                 for (size_t i = g0; i < n / 4; i += stride) dst[i] = src[i];
                 for (size_t i = (n / 4) * 4 + g0; i < n; i += stride) bufs.p[SEL_OUT][i] = bufs.p[SEL_IN][i];
@@ -855,9 +860,9 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
     const uint32_t lbits = sp->segbits - gbits, lmask = (1u << lbits) - 1u;
     const uint32_t climit = sp->maxt << lbits;
 
-    for (uint32_t i = tid; i < (uint32_t)(W * R); i += OSP_BLOCK) sm.wh[i] = 0u;
+    for (uint32_t i = tid; i < (uint32_t)(W * R); i += BLK) sm.wh[i] = 0u;
     if constexpr (LBASE)
-        for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += OSP_BLOCK) sm.base[i] = sp->base[i];
+        for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += BLK) sm.base[i] = sp->base[i];
     const __amdgpu_buffer_rsrc_t rin = osp_rsrc(in, n), rout = osp_rsrc(out, n);
     const __amdgpu_buffer_rsrc_t rvin = osp_rsrc(KV ? vbufs.p[srcsel] : in, n),
                                  rvout = osp_rsrc(KV ? vbufs.p[plan->dst[pass]] : out, n);
@@ -1231,7 +1236,7 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             if (OSP_BUF) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
+                    const uint32_t i = (uint32_t)j * BLK + tid;
                     const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
                     // a partial tile's sentinels (i >= nvalidA) go past the array's end: dropped
                     const uint32_t dst = i < nvalidA ? sm.delta[((key ^ flip) >> shift) & 255u] + i : n;
@@ -1242,14 +1247,14 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
             } else if (nvalidA == (uint32_t)TILE) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
+                    const uint32_t i = (uint32_t)j * BLK + tid;
                     const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
                     osp_store(out + sm.delta[((key ^ flip) >> shift) & 255u] + i, key);
                 }
             } else {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = (uint32_t)j * OSP_BLOCK + tid;
+                    const uint32_t i = (uint32_t)j * BLK + tid;
                     const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
                     if (i < nvalidA) osp_store(out + sm.delta[((key ^ flip) >> shift) & 255u] + i, key);
                 }
@@ -1292,11 +1297,11 @@ __global__ __launch_bounds__(OSP_BLOCK, OSP_BLOCKS_PER_CU * OSP_BLOCK / 256) voi
         OSP_T(8, 0);  // reorder
         if (!OSP_LDS_SCATTER) {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * OSP_BLOCK + tid)];
+            for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * BLK + tid)];
         }
         if constexpr (KV && !LDSV) {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) vA[j] = sm.vals[osp_pad(j * OSP_BLOCK + tid)];
+            for (int j = 0; j < KPT; ++j) vA[j] = sm.vals[osp_pad(j * BLK + tid)];
         }
         // each wave clears its own counters (no barrier before the next ranking)
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
@@ -1932,7 +1937,7 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
     }
     if (vb) {  // key/value: the default variant (lane-ordered atomic rank) only
         if constexpr (OSP_TILE <= 16384) {  // keys + payloads in LDS: 16384-pair tiles at most
-            k_onesweep_p<2, false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback,
+            k_onesweep_p<2, false, true><<<g, OSP_KV_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback,
                                                                  counter, err, *vb);
             return hipGetLastError();
         }
