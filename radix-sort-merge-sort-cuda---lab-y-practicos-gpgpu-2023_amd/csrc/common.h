@@ -155,6 +155,19 @@ struct MgPairs {
 #endif
 constexpr int MG_BRACKET = LABSORT_MG_BRACKET;  // co-rank search: every 8th tile first, the rest bracketed
 constexpr int MG_BLOCKS_PER_CU = LABSORT_MG_BPC;  // persistent merge pass grid
+// co-rank searches by lane groups (k-ary: fewer dependent load rounds) instead of one
+// binary search per thread
+#ifndef LABSORT_MG_KARY
+#define LABSORT_MG_KARY 0
+#endif
+constexpr bool MG_KARY = LABSORT_MG_KARY != 0;
+#ifndef LABSORT_MG_K1
+#define LABSORT_MG_K1 64  // lanes per round-1 search
+#endif
+#ifndef LABSORT_MG_K2
+#define LABSORT_MG_K2 16  // lanes per round-2 (bracketed) search
+#endif
+constexpr int MG_K1 = LABSORT_MG_K1, MG_K2 = LABSORT_MG_K2;
 
 // ---- K-way merge (kmerge.hip) ----
 // (overridable for diagnostic builds under harness/exp)

@@ -26,6 +26,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 namespace labsort {
 
@@ -1572,6 +1573,35 @@ __device__ __forceinline__ uint32_t corank(const uint32_t *A, uint32_t la, const
     return lo;
 }
 
+// The same co-rank by a group of K consecutive lanes (K divides 64): each round the
+// group probes K points of [lo, hi) at once and keeps the interval between the last
+// probe where A's key goes first and the next one, so a search over 2^27 keys takes
+// 5 dependent rounds of loads at K = 64 (4 at K = 16 over a 32K-key bracket) instead
+// of 27.  Every lane of the wave calls it (ballots); `live`: this group searches.
+template <int K>
+__device__ __forceinline__ uint32_t corank_group(const uint32_t *A, uint32_t la, const uint32_t *B, uint32_t lb,
+                                                 uint32_t diag, uint32_t flip, uint32_t lo, uint32_t hi, bool live) {
+    const uint32_t lane = threadIdx.x & 63u, sub = lane & (uint32_t)(K - 1), gbase = lane & ~(uint32_t)(K - 1);
+    if (diag > lb && lo < diag - lb) lo = diag - lb;
+    if (hi > diag) hi = diag;
+    if (hi > la) hi = la;
+    if (!live) lo = hi = 0u;
+    while (__ballot(lo < hi) != 0ull) {
+        const uint32_t span = hi - lo;
+        const uint32_t p = lo + (uint32_t)(((uint64_t)(sub + 1u) * span) / (uint64_t)(K + 1));
+        const bool pred = lo < hi && key_le(A[p], B[diag - 1u - p], flip);
+        const uint64_t bal = __ballot(pred) >> gbase;
+        const uint32_t c = (uint32_t)__popcll(K == 64 ? bal : (bal & ((1ull << (K & 63)) - 1ull)));
+        if (lo < hi) {  // the probes' predicate is true on a prefix of them (c probes)
+            const uint32_t nlo = c ? lo + (uint32_t)(((uint64_t)c * span) / (uint64_t)(K + 1)) + 1u : lo;
+            const uint32_t nhi = c < (uint32_t)K ? lo + (uint32_t)(((uint64_t)(c + 1u) * span) / (uint64_t)(K + 1)) : hi;
+            lo = nlo;
+            hi = nhi;
+        }
+    }
+    return lo;
+}
+
 template <bool KV = false>
 struct MgSmem {
     uint32_t in[MG_TILE];
@@ -1688,12 +1718,60 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         }
         return corank(src + g.pb, g.la, src + g.pb + g.la, g.lb, o - g.pb, flip, lo, hi);
     };
-    for (uint32_t i = tid * MG_BRACKET; i <= nb; i += BLOCK * MG_BRACKET) s_part[i] = search(i, 0);
-    if (tid == 0 && nb % MG_BRACKET) s_part[nb] = search(nb, 0);
-    __syncthreads();
-    for (uint32_t i = tid; i < nb; i += BLOCK)
-        if (i % MG_BRACKET) s_part[i] = search(i, MG_BRACKET);
-    __syncthreads();
+    if constexpr (MG_KARY) {
+        // the same two rounds with lane-group searches: round 1 one wave per co-rank (64
+        // probes per load round), round 2 one 16-lane group per co-rank inside its bracket
+        auto group_search = [&](uint32_t i, uint32_t S, bool live, auto kc) {
+            constexpr int K = decltype(kc)::value;
+            const uint32_t o = (t0 + i) * T;
+            live = live && o < n;
+            const PairGeom g = live ? pair_of(o, n, run, pr) : PairGeom{0u, 0u, 0u};
+            uint32_t lo = 0u, hi = ~0u;
+            if (live && S) {
+                const uint32_t il = i - i % S, ih = il + S < nb ? il + S : nb;
+                const uint32_t ol = (t0 + il) * T, oh = (t0 + ih) * T;
+                if (pair_of(ol, n, run, pr).pb == g.pb) {
+                    lo = s_part[il];
+                    hi = lo + (o - ol);
+                }
+                if (oh < n && pair_of(oh, n, run, pr).pb == g.pb) {
+                    const uint32_t ah = s_part[ih];
+                    hi = hi < ah ? hi : ah;
+                    if (ah > oh - o && lo < ah - (oh - o)) lo = ah - (oh - o);
+                }
+            }
+            return corank_group<K>(src + g.pb, g.la, src + g.pb + g.la, g.lb, live ? o - g.pb : 0u, flip, lo, hi, live);
+        };
+        constexpr uint32_t NWV = BLOCK / MG_K1, NG = BLOCK / MG_K2;  // round 1 / round 2 searches at once
+        const uint32_t wv = tid / MG_K1, lane = tid & 63u;
+        const uint32_t r1 = nb / MG_BRACKET + 1u + (nb % MG_BRACKET ? 1u : 0u);  // i = 0, S, 2S, ... and nb
+        for (uint32_t k = 0; k * NWV < r1; ++k) {
+            const uint32_t e = k * NWV + wv;
+            const uint32_t i = e * MG_BRACKET <= nb ? e * MG_BRACKET : nb;
+            const uint32_t a = group_search(i, 0u, e < r1, std::integral_constant<int, MG_K1>{});
+            if (e < r1 && lane % MG_K1 == 0u) s_part[i] = a;
+        }
+        __syncthreads();
+        for (uint32_t k = 0; k * NG < nb; ++k) {
+            const uint32_t i = k * NG + tid / MG_K2;
+            const uint32_t a = group_search(i, MG_BRACKET, i < nb && (i % MG_BRACKET) != 0u, std::integral_constant<int, MG_K2>{});
+            if (i < nb && (i % MG_BRACKET) != 0u && tid % MG_K2 == 0u) s_part[i] = a;
+        }
+        __syncthreads();
+    } else {
+        for (uint32_t i = tid * MG_BRACKET; i <= nb; i += BLOCK * MG_BRACKET) s_part[i] = search(i, 0);
+        if (tid == 0 && nb % MG_BRACKET) s_part[nb] = search(nb, 0);
+        __syncthreads();
+        for (uint32_t i = tid; i < nb; i += BLOCK)
+            if (i % MG_BRACKET) s_part[i] = search(i, MG_BRACKET);
+        __syncthreads();
+    }
+#ifdef LABSORT_MG_DIAG_PROLOGUE
+    if (LABSORT_MG_DIAG_PROLOGUE == 1 || (LABSORT_MG_DIAG_PROLOGUE == 2 && n == 0xFFFFFFFFu)) {  // timing build: co-ranks only
+        if (tid == 0 && s_part[0] == 0xFFFFFFFFu) dst[0] = 0u;
+        return;
+    }
+#endif
     struct Geo {
         uint32_t o0, tot, la, sa, sb;  // output start, keys, A keys, A start, B start (absolute)
     };
