@@ -215,8 +215,9 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
         HIP_TRY(launch_plan8(hps, joint, n, in == out ? 1 : 0, plan, sps, hist, s));
         for (int p = 0; p < L.P; ++p) {
             TimingScope ts(LABSORT_K_ONESWEEP, s);
+            // (LABSORT_OSP_JCOUNT timing builds count into hps, free once the plan is built)
             HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
-                                      counters + (size_t)p * OSP_NCTR, err, s));
+                                      counters + (size_t)p * OSP_NCTR, err, s, nullptr, LABSORT_OSP_JCOUNT ? hps : nullptr));
         }
     } else {
         HIP_TRY(launch_zero(ws, L.zero_bytes, s));

@@ -63,6 +63,9 @@ constexpr int OSP_TILE = OSP_BLOCK * OSP_KPT;  // 16384 keys per tile
 #define LABSORT_OSP_KV_BLOCK 512  // r26: 0.902 vs 0.939 ms per pair pass (1024 x 16); with the prefetch 1.020
 #endif
 constexpr int OSP_KV_BLOCK = LABSORT_OSP_KV_BLOCK;
+#ifndef LABSORT_OSP_JCOUNT
+#define LABSORT_OSP_JCOUNT 0  // timing build: in-pass joint counting (kernels.hip)
+#endif
 constexpr int OSP_LBW = LABSORT_OSP_LBW;    // look-back window of the first round (predecessor tiles)
 constexpr int OSP_LBW2 = LABSORT_OSP_LBW2;  // look-back window of the later rounds
 constexpr bool OSP_PREFETCH = LABSORT_OSP_PREFETCH != 0;  // next tile's keys loaded one iteration ahead
@@ -296,7 +299,7 @@ hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, in
                         SegPlan *segplans, uint32_t *hist, hipStream_t s);
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
                              uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s,
-                             const Bufs *vb = nullptr);
+                             const Bufs *vb = nullptr, uint32_t *jout = nullptr);
 hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);

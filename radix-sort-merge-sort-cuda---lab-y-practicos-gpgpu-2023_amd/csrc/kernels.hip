@@ -733,6 +733,9 @@ constexpr bool OSP_2BAR = LABSORT_OSP_2BAR != 0;
 // digit offsets, while the other waves issue A's scatter: no cross-wave scan, so the
 // aggregate's barrier (2b) goes (three barriers per tile).  Keys-only passes with the
 // histogram after the rank (the default variant).
+// LABSORT_OSP_JCOUNT (timing build): each pass also counts (top nibble of its digit,
+// next active digit) per key in LDS and flushes the 4096 counts with device atomics at
+// exit -- what counting the next pass's segment histograms in the pass would cost
 #ifndef LABSORT_OSP_W0SCAN
 #define LABSORT_OSP_W0SCAN 0
 #endif
@@ -769,6 +772,7 @@ struct OspSmem {
     uint32_t woff[OSP_2BAR && !KV ? W * R : 1];  // two-barrier loop: each wave's digit offsets
     uint32_t agg[(OSP_2BAR || OSP_W0SCAN) && !KV ? R : 1];   // two-barrier / wave-0 scan: B's tile
     uint32_t dst0[(OSP_2BAR || OSP_W0SCAN) && !KV ? R : 1];  //   histogram and digit starts
+    uint32_t jh[LABSORT_OSP_JCOUNT && !KV ? 4096 : 1];       // in-pass joint counts (timing build)
     uint32_t start[NSEG + 1];
     uint32_t tpre[NSEG + 1];
     uint32_t wsum[8];
@@ -798,7 +802,7 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                              OSP_BLOCKS_PER_CU *(KV ? OSP_KV_BLOCK : OSP_BLOCK) / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
                                                           uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
                                                           uint32_t *lookback, uint32_t *counter, uint32_t *err,
-                                                          Bufs vbufs) {
+                                                          Bufs vbufs, uint32_t *jout = nullptr) {
     using S = OspSmem<RANK != OSP_RANK_BALLOT, KV>;
 #ifndef LABSORT_OSP_KV_PF
 #define LABSORT_OSP_KV_PF 0  // r26 A/B at 2^28 pairs: 0.830 ms per pass without, 1.018 with (27 VGPRs spilled)
@@ -862,6 +866,11 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
     const uint32_t climit = sp->maxt << lbits;
 
     for (uint32_t i = tid; i < (uint32_t)(W * R); i += BLK) sm.wh[i] = 0u;
+    constexpr bool JC = LABSORT_OSP_JCOUNT && !KV;
+    const uint32_t jnext = JC && jout ? plan->next[pass] : NEXT_NONE;
+    const uint32_t jshift = 8u * (jnext & 3u);
+    if constexpr (JC)
+        for (uint32_t i = tid; i < 4096u; i += BLK) sm.jh[i] = 0u;
     if constexpr (LBASE)
         for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += BLK) sm.base[i] = sp->base[i];
     const __amdgpu_buffer_rsrc_t rin = osp_rsrc(in, n), rout = osp_rsrc(out, n);
@@ -1057,6 +1066,11 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
+                if (JC && jnext != NEXT_NONE) {  // (sentinels count into a bin no segment plan reads: nibble 15, digit 255)
+                    const uint32_t x = kB[j] ^ flip;
+                    __hip_atomic_fetch_add(&sm.jh[((d & 0xF0u) << 4) | ((x >> jshift) & 255u)], 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
                 if (atomic_rank) {
                     const uint32_t r = wave_atomic_rank(wh, d, lane);
                     rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
@@ -1323,6 +1337,14 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
             cC = sm.next;
         } else {
             cB = sm.next;
+        }
+    }
+    if (JC && jnext != NEXT_NONE) {
+        __syncthreads();
+        const uint32_t rot = (blockIdx.x * 64u) & 4095u;
+        for (uint32_t i0 = tid; i0 < 4096u; i0 += BLK) {
+            const uint32_t i = (i0 + rot) & 4095u, c = sm.jh[i];
+            if (c) atomicAdd(jout + i, c);
         }
     }
 #ifdef OSP_STAMPS
@@ -2004,7 +2026,8 @@ static int cu_count() {
 }
 
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
-                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s, const Bufs *vb) {
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s, const Bufs *vb,
+                             uint32_t *jout) {
     const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE + NSEG;
     const size_t want = (size_t)OSP_BLOCKS_PER_CU * cu_count();
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
@@ -2026,7 +2049,7 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
     case 1: k_onesweep_p<0, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
     case 2: k_onesweep_p<1, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
     case 3: k_onesweep_p<1, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
-    case 4: k_onesweep_p<2, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
+    case 4: k_onesweep_p<2, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b, jout); break;
     case 5: k_onesweep_p<2, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
     default: return hipErrorInvalidValue;
     }
