@@ -624,6 +624,52 @@ def main():
                    "verified": "sorted permutation (descents, digit histograms, sums)"}
         del s2, o2, w2
 
+    # SURVEY 8f row 4 beside the headline: the stable key/value radix sort of the same keys
+    # with 4-byte payloads (each its input index), verified as the pairs run is
+    pairs_leg = None
+    if world == 1 and args.algo == "radix" and not args.no_merge:
+        vin = torch.arange(n, dtype=torch.int32, device=dev)
+        pko = torch.empty_like(src)
+        pvo = torch.empty_like(src)
+        pws = torch.empty(max(ls.pairs_workspace_bytes(n, "radix"), 256), dtype=torch.uint8, device=dev)
+
+        def pstep():
+            ls.sort_pairs_device(src, vin, pko, pvo, n, key=key, algo="radix", workspace=pws, stream=stream)
+
+        for _ in range(args.warmup):
+            pstep()
+        torch.cuda.synchronize()
+        ls.timing_enable(True)
+        p0 = time.perf_counter()
+        for _ in range(args.steps):
+            pstep()
+        torch.cuda.synchronize()
+        p1 = time.perf_counter()
+        pp_ms, pp_cnt = ls.timing_read("onesweep")
+        ls.timing_enable(False)
+        ls.pairs_workspace_status(pws, n, "radix", stream=stream)
+        pok, _ = verify(torch, ls, src, pko, n, key)
+        if pok:
+            idx = pvo.to(torch.int64)
+            pok = bool((idx >= 0).all()) and bool((idx < n).all()) and torch.equal(src[idx], pko)
+            if pok and n > 1:
+                pok = bool(((pvo[1:] > pvo[:-1]) | (pko[1:] != pko[:-1])).all())
+            del idx
+        if not pok:
+            print("bench.py: KEY/VALUE OUTPUT CHECK FAILED", file=sys.stderr)
+            sys.exit(3)
+        pavg = pp_ms / pp_cnt if pp_cnt else None
+        pairs_leg = {"workload": f"stable key/value LSD radix (4-byte payloads) of the same 2^{args.log2n} keys",
+                     "value": round(n * args.steps / (p1 - p0) / 1e6, 2), "unit": "Mpairs/s",
+                     "ms_per_step": round((p1 - p0) / args.steps * 1e3, 4),
+                     "verified": "sorted, payload = input index of its key, equal keys in input order",
+                     "roofline": {"bound": "hbm", "kernel": "k_onesweep_p<2, false, true>", "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "avg_launch_ms": round(pavg, 5) if pavg else None,
+                                  "achieved": round(16.0 * n / (pavg * 1e-3) / 1e9, 1) if pavg else None,
+                                  "frac": round(16.0 * n / (pavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pavg else None,
+                                  "algorithmic_bytes_per_launch": 16.0 * n}}
+        del vin, pko, pvo, pws
+
     config1 = None
     if world == 1 and args.algo == "radix" and not args.no_merge:
         config1 = config1_gpu(ls, torch, dev, stream)
@@ -716,6 +762,8 @@ def main():
             line["config1"] = config1
         if config2:
             line["config2"] = config2
+        if pairs_leg:
+            line["pairs"] = pairs_leg
         if xgmi:
             line["config"]["local_algo"] = "radix"
             line["xgmi"] = xgmi
