@@ -681,6 +681,9 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
 // cycles it spends in each phase of the tile loop and adds them into g_osp_stamps at
 // exit; labsort_exp_stamps reads them.  OSP_T(i, w) closes phase i after waiting for
 // (w & 1) global memory / (w & 2) LDS operations to complete.
+#ifndef OSP_STAMP_W0
+#define OSP_STAMP_W0 1
+#endif
 #ifdef OSP_STAMPS
 __device__ unsigned long long g_osp_stamps[16];
 #define OSP_T(i, w)                                                              \
@@ -1048,7 +1051,7 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                 if ((uint32_t)j * WAVE + wid * (KPT * WAVE) + lane < nvalidB)
                     atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
         }
-        OSP_T(0, 1);  // look-back issue + B's keys landed
+        OSP_T(0, OSP_STAMP_W0);  // look-back issue + B's keys landed (OSP_STAMP_W0 = 0: issue only)
         if constexpr (HIST_FIRST) __syncthreads();  // (1) histogram of B complete
         if (haveB) {
             if (HIST_FIRST && tid < (uint32_t)R) {
