@@ -731,6 +731,13 @@ constexpr bool OSP_BUF = LABSORT_OSP_BUF != 0;
 #define LABSORT_OSP_2BAR 0
 #endif
 constexpr bool OSP_2BAR = LABSORT_OSP_2BAR != 0;
+// LABSORT_OSP_ST4: each lane scatters groups of 4 consecutive sorted slots; a group within
+// one digit run (4 consecutive destinations) is one 16-B store, a group spanning a run
+// edge or the tile's end falls back to 4-B stores.  A quarter of the store instructions
+// carry the bulk of the keys (the pass's issue is paced by the memory queue).
+#ifndef LABSORT_OSP_ST4
+#define LABSORT_OSP_ST4 1  // r26: 0.472 -> 0.464 ms per pass (uniform), 0.474 -> 0.454 (sorted)
+#endif
 // LABSORT_OSP_W0SCAN: wave 0 alone sums B's 16 wave counts (4 digits per lane, 16-B LDS
 // reads), scans them with one wave scan, publishes B's aggregate and writes every wave's
 // digit offsets, while the other waves issue A's scatter: no cross-wave scan, so the
@@ -831,6 +838,8 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
     static_assert(!KV || OSP_BUF, "key/value passes use the buffer-descriptor loads and stores");
     constexpr int R = S::R, W = S::W, TILE = S::TILE, BLK = S::BLOCK, KPT = TILE / BLK, LBW = OSP_LBW, LBW2 = OSP_LBW2;
     static_assert(BLK >= 512 && R <= BLK && NSEG == 16 && KPT * BLK == TILE, "digit threads = waves 0-3; c & 15 = segment");
+    // (key/value: 0.865-0.900 vs 0.843-0.853 ms per pass with it, profiles/r26_ab_st4.txt)
+    constexpr bool ST4 = LABSORT_OSP_ST4 && OSP_BUF && !KV && !OSP_LDS_SCATTER && KPT % 4 == 0;
     __shared__ S sm;
 
     const uint32_t srcsel = plan->src[pass];
@@ -1251,7 +1260,33 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
             }
         }
         if (slotA != OSP_DONE) {
-            if (OSP_BUF) {
+            if (ST4) {
+#pragma unroll
+                for (int g = 0; g < KPT / 4; ++g) {
+                    const uint32_t i0 = 4u * ((uint32_t)g * BLK + tid);  // slots i0 .. i0 + 3
+                    uint32_t d[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) d[q] = ((kA[4 * g + q] ^ flip) >> shift) & 255u;
+                    const bool whole = d[0] == d[3] && i0 + 3u < nvalidA;  // sorted: d0 == d3 => all equal
+                    const uint32_t dst0 = sm.delta[d[0]] + i0;
+                    if (whole) {
+                        const u32x4 v = {kA[4 * g], kA[4 * g + 1], kA[4 * g + 2], kA[4 * g + 3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(v, rout, dst0 * 4u, 0, 0);
+                        if constexpr (KV) {
+                            const u32x4 w = {vA[4 * g], vA[4 * g + 1], vA[4 * g + 2], vA[4 * g + 3]};
+                            __builtin_amdgcn_raw_buffer_store_b128(w, rvout, dst0 * 4u, 0, 0);
+                        }
+                    } else {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const uint32_t i = i0 + (uint32_t)q;
+                            const uint32_t dst = i < nvalidA ? sm.delta[d[q]] + i : n;
+                            __builtin_amdgcn_raw_buffer_store_b32(kA[4 * g + q], rout, dst * 4u, 0, 0);
+                            if constexpr (KV) __builtin_amdgcn_raw_buffer_store_b32(vA[4 * g + q], rvout, dst * 4u, 0, 0);
+                        }
+                    }
+                }
+            } else if (OSP_BUF) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t i = (uint32_t)j * BLK + tid;
@@ -1313,11 +1348,20 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
         }
         __syncthreads();  // (4) B reordered in LDS
         OSP_T(8, 0);  // reorder
-        if (!OSP_LDS_SCATTER) {
+        if (ST4) {  // slots 4 (g BLK + tid) + q, q = 0..3 (never across a pad word)
+#pragma unroll
+            for (int g = 0; g < KPT / 4; ++g)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t at = osp_pad(4u * ((uint32_t)g * BLK + tid) + (uint32_t)q);
+                    kA[4 * g + q] = sm.keys[at];
+                    if constexpr (KV) vA[4 * g + q] = sm.vals[at];
+                }
+        } else if (!OSP_LDS_SCATTER) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * BLK + tid)];
         }
-        if constexpr (KV && !LDSV) {
+        if constexpr (KV && !LDSV && !ST4) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) vA[j] = sm.vals[osp_pad(j * BLK + tid)];
         }
