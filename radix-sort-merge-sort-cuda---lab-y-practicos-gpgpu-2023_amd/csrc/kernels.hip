@@ -1858,7 +1858,36 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         q.sb = g.pb + g.la + b0;
         return q;
     };
+#ifndef LABSORT_MG_LD4
+#define LABSORT_MG_LD4 0
+#endif
+    // LD4: thread keeps tile slots 4 (j BLOCK/4 + tid) + q, loaded as one 16-B load when the
+    // four lie in one run (A or B) and the tile (else four 4-B loads)
+    constexpr bool LD4 = LABSORT_MG_LD4 && !KV && KPT % 4 == 0;
     auto load = [&](const Geo &q, uint32_t (&v)[KPT], uint32_t (&vv)[KV ? KPT : 1]) {
+        if constexpr (LD4) {
+#pragma unroll
+            for (int j = 0; j < KPT / 4; ++j) {
+                const uint32_t k0 = 4u * (tid + (uint32_t)j * BLOCK);
+                if (k0 + 3u < q.tot && (k0 + 3u < q.la || k0 >= q.la)) {
+                    const uint32_t a = k0 < q.la ? q.sa + k0 : q.sb + (k0 - q.la);
+                    uint32_t w[4];
+                    __builtin_memcpy(w, src + a, 16);  // (4-B aligned: one 16-B load)
+                    v[4 * j] = w[0];
+                    v[4 * j + 1] = w[1];
+                    v[4 * j + 2] = w[2];
+                    v[4 * j + 3] = w[3];
+                } else {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const uint32_t k = k0 + (uint32_t)u;
+                        const uint32_t a = k < q.la ? q.sa + k : q.sb + (k - q.la);
+                        v[4 * j + u] = k < q.tot ? src[a] : 0u;
+                    }
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t k = tid + (uint32_t)j * BLOCK;
@@ -1873,8 +1902,15 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
     load(cur, nx, nv);
     for (uint32_t t = t0; t < t1; ++t) {
         __syncthreads();  // previous tile's merge no longer reads sm.in
+        if constexpr (LD4) {
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
+            for (int j = 0; j < KPT / 4; ++j)
+                *reinterpret_cast<uint4 *>(sm.in + 4u * (tid + (uint32_t)j * BLOCK)) =
+                    make_uint4(nx[4 * j], nx[4 * j + 1], nx[4 * j + 2], nx[4 * j + 3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
+        }
         if constexpr (KV) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) sm.vin[tid + (uint32_t)j * BLOCK] = nv[j];
