@@ -840,6 +840,12 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
     static_assert(BLK >= 512 && R <= BLK && NSEG == 16 && KPT * BLK == TILE, "digit threads = waves 0-3; c & 15 = segment");
     // (key/value: 0.865-0.900 vs 0.843-0.853 ms per pass with it, profiles/r26_ab_st4.txt)
     constexpr bool ST4 = LABSORT_OSP_ST4 && OSP_BUF && !KV && !OSP_LDS_SCATTER && KPT % 4 == 0;
+#ifndef LABSORT_OSP_LD4
+#define LABSORT_OSP_LD4 0
+#endif
+    // LD4: 16-B key loads in the first active pass of keys-only sorts (see load_tile)
+    constexpr bool LD4 = LABSORT_OSP_LD4 && OSP_BUF && !KV && KPT % 4 == 0;
+    const bool ld4_pass = LD4 && plan->prev[pass] == NEXT_NONE;
     __shared__ S sm;
 
     const uint32_t srcsel = plan->src[pass];
@@ -975,7 +981,20 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
         const uint32_t *src = in + beg + woff;
         if constexpr (OSP_BUF) {  // out-of-range offsets read 0 (replaced by the sentinel)
             const uint32_t o = (beg + woff) * 4u;
-            if (nv == (uint32_t)TILE) {
+            if (LD4 && ld4_pass && nv == (uint32_t)TILE) {
+                // first active pass of a keys-only sort: the order of equal digits within a
+                // tile is free (nothing earlier to keep), so each lane loads 4 consecutive keys
+                // per 256-key chunk with one 16-B load and ranks them as its slots
+                const uint32_t o4 = (beg + wid * (KPT * WAVE) + 4u * lane) * 4u;
+#pragma unroll
+                for (int q = 0; q < KPT / 4; ++q) {
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rin, o4 + q * 4 * WAVE * 4, 0, OSP_BUF_NT);
+                    k[4 * q] = v.x;
+                    k[4 * q + 1] = v.y;
+                    k[4 * q + 2] = v.z;
+                    k[4 * q + 3] = v.w;
+                }
+            } else if (nv == (uint32_t)TILE) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) k[j] = __builtin_amdgcn_raw_buffer_load_b32(rin, o + j * WAVE * 4, 0, OSP_BUF_NT);
             } else {
