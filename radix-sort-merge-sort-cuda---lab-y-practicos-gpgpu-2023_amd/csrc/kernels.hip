@@ -1460,6 +1460,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
     using S = TsSmem<BLOCK, KPT, KV>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE;
     constexpr int PFK = KV ? 0 : (LABSORT_TS_PFK < KPT ? LABSORT_TS_PFK : KPT);
+#ifndef LABSORT_TS_V4
+#define LABSORT_TS_V4 0
+#endif
+    constexpr bool V4 = LABSORT_TS_V4 && !KV && PFK == 0 && KPT % 4 == 0;
     __shared__ S sm;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t sentinel = ~flip;
@@ -1477,6 +1481,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
         uint32_t v[KV ? KPT : 1];
         uint32_t a = ~0u, o = 0u;
         const bool full = base + (uint32_t)TILE <= n;  // no bounds checks (one base address)
+        const bool g4 = V4 && full && ((((uintptr_t)in) | ((uintptr_t)out)) & 15u) == 0u;  // grouped 16-B I/O
         if constexpr (KV) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
@@ -1484,7 +1489,25 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
                 v[j] = idx < n ? vin[idx] : 0u;
             }
         }
-        if (full) {
+        // V4 (keys only, full tiles): 16-B loads, each lane 4 consecutive keys per 256-key
+        // chunk ("grouped" order: the first pass may rank equal digits in any order), and
+        // after the last pass a grouped read-back, so the tile leaves as 16-B stores
+        const uint32_t gbase = base + wid * (KPT * WAVE) + 4u * lane;  // + 256 q + s
+        if (g4) {
+#pragma unroll
+            for (int q = 0; q < KPT / 4; ++q) {
+                const uint4 x = *reinterpret_cast<const uint4 *>(in + gbase + 256u * q);
+                k[4 * q] = x.x;
+                k[4 * q + 1] = x.y;
+                k[4 * q + 2] = x.z;
+                k[4 * q + 3] = x.w;
+            }
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                a &= k[j] ^ flip;
+                o |= k[j] ^ flip;
+            }
+        } else if (full) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j)
                 k[j] = (j < PFK && have_pf) ? pf[j < PFK ? j : 0] : ld_stream<NT_TILE>(in + wbase + j * WAVE);
@@ -1587,14 +1610,29 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
                 if constexpr (KV) sm.vals[dst] = v[j];
             }
             __syncthreads();
+            if (g4 && pass == last) {  // grouped read-back (16-B LDS reads, conflict-free)
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
+                for (int q = 0; q < KPT / 4; ++q) {
+                    const uint4 x = *reinterpret_cast<const uint4 *>(sm.keys + wid * (KPT * WAVE) + 4u * lane + 256u * q);
+                    k[4 * q] = x.x;
+                    k[4 * q + 1] = x.y;
+                    k[4 * q + 2] = x.z;
+                    k[4 * q + 3] = x.w;
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
+            }
             if constexpr (KV) {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) v[j] = sm.vals[wid * (KPT * WAVE) + j * WAVE + lane];
             }
         }
-        if (full) {
+        if (g4) {
+#pragma unroll
+            for (int q = 0; q < KPT / 4; ++q)
+                *reinterpret_cast<uint4 *>(out + gbase + 256u * q) = make_uint4(k[4 * q], k[4 * q + 1], k[4 * q + 2], k[4 * q + 3]);
+        } else if (full) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
         } else {
