@@ -754,6 +754,9 @@ constexpr bool OSP_W0SCAN = LABSORT_OSP_W0SCAN != 0;
 #define LABSORT_OSP_EARLY_ACQ 1  // r26: 0.4906 -> 0.4729 ms per pass at 2^28 (barrier 3: 11.9 -> 7.1 % of wave time)
 #endif
 constexpr bool OSP_EARLY_ACQ = LABSORT_OSP_EARLY_ACQ != 0;
+#ifndef LABSORT_OSP_MATCH
+#define LABSORT_OSP_MATCH 1  // the LDS match buffer for the rank's fallback (0: 8-ballot fallback)
+#endif
 #ifndef LABSORT_OSP_LBASE
 #define LABSORT_OSP_LBASE 1  // the segments' output bases in LDS (else read from the SegPlan)
 #endif
@@ -773,7 +776,7 @@ struct OspSmem {
     uint32_t keys[TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0)];  // padded: see osp_pad
     uint32_t vals[KV ? TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0) : 1];  // key/value: payloads, reordered alike
     uint32_t wh[W * R];
-    uint64_t match[MATCH && !KV && OSP_TILE <= 16384 ? W * R : 1];  // (no room beside bigger tiles)
+    uint64_t match[MATCH && !KV && OSP_TILE <= 16384 && LABSORT_OSP_MATCH ? W * R : 1];  // (no room beside bigger tiles)
     uint32_t probe[WAVE];
     uint32_t ordered;
     uint32_t hist[R];
@@ -1106,7 +1109,7 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                     const uint32_t r = wave_atomic_rank(wh, d, lane);
                     rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
                 } else {
-                    const uint64_t m = (RANK != OSP_RANK_BALLOT && !KV && OSP_TILE <= 16384) ? lds_peers(wm + d, lane)
+                    const uint64_t m = (RANK != OSP_RANK_BALLOT && !KV && OSP_TILE <= 16384 && LABSORT_OSP_MATCH) ? lds_peers(wm + d, lane)
                                                                                           : match8(d);
                     const uint32_t pre = mbcnt64(m);
                     const uint32_t old = wh[d];
