@@ -842,7 +842,12 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
     constexpr int R = S::R, W = S::W, TILE = S::TILE, BLK = S::BLOCK, KPT = TILE / BLK, LBW = OSP_LBW, LBW2 = OSP_LBW2;
     static_assert(BLK >= 512 && R <= BLK && NSEG == 16 && KPT * BLK == TILE, "digit threads = waves 0-3; c & 15 = segment");
     // (key/value: 0.865-0.900 vs 0.843-0.853 ms per pass with it, profiles/r26_ab_st4.txt)
-    constexpr bool ST4 = LABSORT_OSP_ST4 && OSP_BUF && !KV && !OSP_LDS_SCATTER && KPT % 4 == 0;
+#ifndef LABSORT_OSP_KV_ST4
+#define LABSORT_OSP_KV_ST4 0  // key/value: 1 = keys and payloads grouped (slower, r26), 2 = keys only
+#endif
+    constexpr bool ST4 = LABSORT_OSP_ST4 && OSP_BUF && (!KV || LABSORT_OSP_KV_ST4) && !LDSV && !OSP_LDS_SCATTER &&
+                         KPT % 4 == 0;
+    constexpr bool ST4V = KV && LABSORT_OSP_KV_ST4 == 1;  // payloads as 16-B groups too
 #ifndef LABSORT_OSP_LD4
 #define LABSORT_OSP_LD4 0
 #endif
@@ -1294,9 +1299,13 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                     if (whole) {
                         const u32x4 v = {kA[4 * g], kA[4 * g + 1], kA[4 * g + 2], kA[4 * g + 3]};
                         __builtin_amdgcn_raw_buffer_store_b128(v, rout, dst0 * 4u, 0, 0);
-                        if constexpr (KV) {
+                        if constexpr (ST4V) {
                             const u32x4 w = {vA[4 * g], vA[4 * g + 1], vA[4 * g + 2], vA[4 * g + 3]};
                             __builtin_amdgcn_raw_buffer_store_b128(w, rvout, dst0 * 4u, 0, 0);
+                        } else if constexpr (KV) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q)
+                                __builtin_amdgcn_raw_buffer_store_b32(vA[4 * g + q], rvout, (dst0 + q) * 4u, 0, 0);
                         }
                     } else {
 #pragma unroll
