@@ -473,7 +473,7 @@ def main():
     dom = "onesweep" if args.algo in ("radix", "radix1") or (args.algo == "pairs" and args.pair_algo == "radix") \
         else "merge"
     if args.algo == "radix" and world == 1 and ls.radix_impl(n) == "gather":
-        dom = "gsweep"  # the gathered passes (2^22 < n < 2^26)
+        dom = "gsweep"  # the gathered passes (2^16 <= n < 2^25)
     if args.algo == "radix" and world == 1 and ls.radix_impl(n) == "small":
         dom = "small"  # the single-launch sort (n <= 2^22)
     if world > 1 and args.exchange != "splitters":

@@ -13,7 +13,7 @@ for _ in range(200):
 torch.cuda.synchronize()
 for n in [int(x) for x in os.environ.get("NS", "").split()] or [256, 4096, 32768, 32769, 49152, 65536, 98304, 131072, 196608, 262144, 524288, 1 << 20, 1 << 21, 1 << 22, 1 << 23]:
     d = torch.empty(n, dtype=torch.int32, device="cuda")
-    ls.fill(d, n, 0x5EED0002, "u32")
+    ls.fill(d, n, 0x5EED0002, os.environ.get("DIST", "u32"), param=int(os.environ.get("PARAM", "0")))
     o = torch.empty_like(d)
     row = {"n": n}
     ref = torch.sort(d.to(torch.int64) & 0xFFFFFFFF)[0].to(torch.int32)

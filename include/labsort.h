@@ -41,7 +41,7 @@ extern "C" {
 #define LABSORT_ERR_DEVICE 3     /* a kernel reported an internal error (bounded spin expired) */
 
 /* algorithms */
-#define LABSORT_ALGO_RADIX 0     /* LSD radix, 8-bit digits: gathered passes for 2^16 <= n < 2^26,
+#define LABSORT_ALGO_RADIX 0     /* LSD radix, 8-bit digits: gathered passes for 2^16 <= n < 2^25,
                                     onesweep scatter passes outside (LABSORT_RADIX_IMPL=onesweep or
                                     =gather forces one; =small: one cooperative launch for
                                     labsort_tile_keys() < n <= 2^22, small.hip) */
@@ -74,7 +74,7 @@ extern "C" {
 #define LABSORT_K_TILE_SORT 2
 #define LABSORT_K_MERGE 3
 #define LABSORT_K_PARTITION 4
-#define LABSORT_K_GSWEEP 5       /* gathered radix pass (LABSORT_ALGO_RADIX, 2^16 <= n < 2^26) */
+#define LABSORT_K_GSWEEP 5       /* gathered radix pass (LABSORT_ALGO_RADIX, 2^16 <= n < 2^25) */
 #define LABSORT_K_GCOPY 6        /* its final gathered copy */
 #define LABSORT_K_SMALL 7        /* single-launch radix sort (LABSORT_ALGO_RADIX, n <= 2^22) */
 #define LABSORT_K_COUNT 8

@@ -375,7 +375,7 @@ def workspace_bytes(n: int, algo: str = "radix") -> int:
     return int(lib.labsort_workspace_bytes(n, ALGO[algo]))
 
 
-GS_MIN_N, GS_MAX_N = 1 << 16, 1 << 26  # LABSORT_ALGO_RADIX's gathered-pass window (common.h)
+GS_MIN_N, GS_MAX_N = 1 << 16, 1 << 25  # LABSORT_ALGO_RADIX's gathered-pass window (common.h)
 SR_MAX_N = 1 << 22  # single-launch radix up to here (common.h SR_MAX_N)
 
 

@@ -3,7 +3,7 @@ LABSORT_RADIX_IMPL, against std::sort (the oracle):
 
   gather    gsweep.hip -- passes gather their tile run by run, sort it in LDS and write
             it contiguously; per-pass run tables; a final gathered copy (the default
-            for 2^16 <= n < 2^26)
+            for 2^16 <= n < 2^25)
   onesweep  kernels.hip k_onesweep_p -- decoupled look-back scatter passes (the
             default outside that window)
 
@@ -101,4 +101,4 @@ def test_gather_pass_structure(ls, oracle, torch_gpu, monkeypatch, mask):
 def test_gather_default_window(ls):
     """which implementation LABSORT_ALGO_RADIX runs, as api.hip decides"""
     assert ls.radix_impl(1 << 15) == "onesweep" and ls.radix_impl(1 << 16) == "gather"
-    assert ls.radix_impl((1 << 26) - 1) == "gather" and ls.radix_impl(1 << 26) == "onesweep"
+    assert ls.radix_impl((1 << 25) - 1) == "gather" and ls.radix_impl(1 << 25) == "onesweep"
