@@ -232,7 +232,7 @@ constexpr int GS_SMALL_NG = LABSORT_GS_SMALL_NG;  // up to this many groups (2^2
 constexpr size_t GS_MIN_N = (size_t)1 << 16;    // LABSORT_ALGO_RADIX uses it for GS_MIN_N <= n < GS_MAX_N
 constexpr size_t GS_MAX_N = (size_t)1 << 25;    // (onesweep outside; r26 crossover at 2^25: 0.420 vs 0.442 ms)
 struct GsLayout {
-    size_t off_state, off_a, off_b, off_rt, off_mm, off_gsx, off_gx, off_gmm, off_ls[2], off_sr[2],
+    size_t off_state, off_a, off_b, off_rt, off_rt2, off_mm, off_gsx, off_gx, off_gmm, off_ls[2], off_sr[2],
         off_first[2], total;
 };
 GsLayout gs_layout(size_t n);

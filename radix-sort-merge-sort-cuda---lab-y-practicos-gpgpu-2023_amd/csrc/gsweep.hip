@@ -32,6 +32,8 @@
 //   ls[e]     logical start of run e (ls[256*ntp] = n)
 //   sr[e]     source address t*TILE + lo(t,d)
 //   first[T]  e of the run holding logical position T*TILE; first[ntp]: position n-1
+#include <algorithm>
+
 #include "../../include/labsort.h"
 #include "common.h"
 #include "devutil.h"
@@ -63,7 +65,13 @@ struct GsState {
 };
 constexpr uint32_t GS_SPIN_LIMIT = 1u << 22;
 
-__device__ __forceinline__ bool gs_active(const GsState *st, int pass) {
+// digit min / max: GsState (written by the scan after pass 0), or GsMM in LDS (the fused
+// small path: every workgroup reduces the tiles' pairs itself)
+struct GsMM {
+    uint32_t dmin[4], dmax[4];
+};
+template <class S>
+__device__ __forceinline__ bool gs_active(const S *st, int pass) {
     return pass == 0 || st->dmin[pass] != st->dmax[pass];
 }
 
@@ -71,19 +79,78 @@ __device__ __forceinline__ bool gs_active(const GsState *st, int pass) {
 // always runs and writes A, every later active pass writes the other buffer.  A
 // function of the digit min / max only (written once, by pass 0's scan), so no kernel
 // ever updates shared "current buffer" state while others read it.
-__device__ __forceinline__ uint32_t gs_cur(const GsState *st, int p) {
+template <class S>
+__device__ __forceinline__ uint32_t gs_cur(const S *st, int p) {
     if (p == 0) return 0u;
     uint32_t nact = 1;
     for (int q = 1; q < p; ++q) nact += st->dmin[q] != st->dmax[q] ? 1u : 0u;
     return (nact & 1u) ? 1u : 2u;
 }
-__device__ __forceinline__ uint32_t gs_dst(const GsState *st, int p) { return gs_cur(st, p) == 1u ? 2u : 1u; }
+template <class S>
+__device__ __forceinline__ uint32_t gs_dst(const S *st, int p) { return gs_cur(st, p) == 1u ? 2u : 1u; }
 
 // tiles dealt per XCD: blocks b, b+8, b+16, ... (one XCD) take consecutive tiles, so a
 // run's neighbouring reads meet in one L2 (bw_probe: gather 0.49 -> 0.44 ms)
 __device__ __forceinline__ uint32_t gs_tile(uint32_t b, uint32_t ntp) {
     const uint32_t per = (ntp + 7u) >> 3;
     return (b & 7u) * per + (b >> 3);
+}
+
+// ---- digit min / max of the tile pairs ------------------------------------------------
+// bytewise min / max of packed digit words (byte q = digit q of key ^ flip)
+__device__ __forceinline__ uint32_t bmin4(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = (a >> (8 * q)) & 255u, y = (b >> (8 * q)) & 255u;
+        r |= (x < y ? x : y) << (8 * q);
+    }
+    return r;
+}
+__device__ __forceinline__ uint32_t bmax4(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = (a >> (8 * q)) & 255u, y = (b >> (8 * q)) & 255u;
+        r |= (x > y ? x : y) << (8 * q);
+    }
+    return r;
+}
+// Wave-wide bytewise min / max of (mn, mx) pairs, result in every lane.
+__device__ __forceinline__ void wave_minmax4(uint32_t &mn, uint32_t &mx) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+        mn = bmin4(mn, __shfl_xor(mn, off));
+        mx = bmax4(mx, __shfl_xor(mx, off));
+    }
+}
+// Digit min / max over `cnt` packed (min, max) pairs into st->dmin / dmax.  Whole
+// block, block-uniform call (barrier).
+template <int BLOCK, class S>
+__device__ __forceinline__ void gs_reduce_minmax(const uint32_t *pairs, uint32_t cnt, uint32_t (*red)[2], S *st) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
+    for (uint32_t i = tid; i < cnt; i += BLOCK) {
+        mn = bmin4(mn, pairs[2 * i]);
+        mx = bmax4(mx, pairs[2 * i + 1]);
+    }
+    wave_minmax4(mn, mx);
+    if (lane == 0) {
+        red[wid][0] = mn;
+        red[wid][1] = mx;
+    }
+    __syncthreads();
+    if (tid < 4u) {
+        uint32_t a = 255u, b = 0u;
+#pragma unroll
+        for (int w = 0; w < BLOCK / WAVE; ++w) {
+            const uint32_t x = (red[w][0] >> (8 * tid)) & 255u, y = (red[w][1] >> (8 * tid)) & 255u;
+            a = x < a ? x : a;
+            b = y > b ? y : b;
+        }
+        st->dmin[tid] = a;
+        st->dmax[tid] = b;
+    }
 }
 
 struct GsRuns {
@@ -175,6 +242,171 @@ __device__ __forceinline__ void gs_gather(const uint32_t *__restrict__ src, cons
     }
 }
 
+// ---- fused small path ------------------------------------------------------------------
+// Up to GS_SMALL_NG scan groups (2^20 keys, 128 tiles: fewer tiles than CUs) the passes
+// are bound by launches, not bytes (r26: ten launches, 0.073-0.080 ms at 2^20).  There
+// the scan is not launched at all: each workgroup of pass p derives the runs of its own
+// tile from the previous pass's tile rows (L2-resident, 1 KB per tile), so a pass is one
+// launch -- sweep 0, sweeps 1-3 and the gathered copy: five launches, no memset.  The
+// rows of a buffer are kept beside it (rt for A, rt2 for B), since the pass that reads
+// A's rows writes B's.
+//
+// LDS of the prologue (aliases the reorder buffer, as GsRuns): run-start bitmap, its
+// popcount prefix, one delta per nonempty run overlapping the tile (at most GT).
+struct GsRunsF {
+    uint32_t bits[GT / 32];
+    uint32_t wpre[GT / 32];
+    int32_t delta[GT];
+    uint32_t wsum[8];
+    uint32_t dlo, dhi, base;
+};
+
+// Fused small path: each active pass q adds its tiles' digit counts into acc[q], spread
+// over GS_FSLOTS copies (tile T into copy T % GS_FSLOTS: 8 atomics per address at 128
+// tiles, where one copy serialised 128 and cost ~5 us a pass).
+constexpr int GS_FSLOTS = 16;
+// after the copies: per copy one 256-B line of pass 0's digit min / max atomics, words
+// 0-3 = 255 - min of digit q, 4-7 = max (zero-initialised maxima)
+constexpr size_t GS_FACC_WORDS = (size_t)4 * GS_FSLOTS * 256, GS_FWORDS = GS_FACC_WORDS + GS_FSLOTS * 64;
+// Start of pass p >= 1 (p = 4: the final copy), one round trip and one barrier: the
+// digit min / max of pass 0 (every thread gets them, in mm) and the digit totals of the
+// logical order before p, for thread tid < 256's digit.  The totals are always read from
+// acc[p - 1]: an active pass accumulates its own there, a skipped pass forwards the
+// totals it received (gs_forward), so no pass has to know which earlier pass wrote them.
+// part: 272 words of LDS.  Block-uniform.
+__device__ __forceinline__ uint32_t gs_fused_prologue(const uint32_t *acc, int p, GsMM &mm, uint32_t *part,
+                                                      uint32_t tid) {
+    static_assert(GB == 512, "two threads per digit");
+    const uint32_t d = tid & 255u, h = tid >> 8, lane = tid & 63u;
+    const uint32_t *a = acc + ((size_t)(p - 1) * GS_FSLOTS + h * (GS_FSLOTS / 2)) * 256 + d;
+    uint32_t v[GS_FSLOTS / 2], c = 0;
+#pragma unroll
+    for (int i = 0; i < GS_FSLOTS / 2; ++i) v[i] = ld_agent(a + i * 256);
+    static_assert(GS_FSLOTS * 8 == 128, "min / max slots: waves 0 and 1");
+    uint32_t m = tid < 128u ? ld_agent(acc + GS_FACC_WORDS + (tid >> 3) * 64u + (tid & 7u)) : 0u;
+#pragma unroll
+    for (int off = 8; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_xor(m, off);
+        m = o > m ? o : m;
+    }
+    if (tid < 128u && lane < 8u) part[256u + (tid >> 6) * 8u + lane] = m;
+#pragma unroll
+    for (int i = 0; i < GS_FSLOTS / 2; ++i) c += v[i];
+    if (h) part[d] = c;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t x = part[256 + q], y = part[264 + q], u = part[260 + q], w = part[268 + q];
+        mm.dmin[q] = 255u - (x > y ? x : y);
+        mm.dmax[q] = u > w ? u : w;
+    }
+    return h ? 0u : c + part[d];
+}
+
+// A skipped pass p: workgroup 0 forwards the totals it received to acc[p] (copy 0; the
+// other copies stay zero), where pass p + 1 (or the final copy) reads them.
+__device__ __forceinline__ void gs_forward(uint32_t *acc, int p, uint32_t tot, uint32_t tid) {
+    if (blockIdx.x == 0 && tid < 256u) acc[(size_t)p * GS_FSLOTS * 256 + tid] = tot;
+}
+
+// Keys of logical tile T (positions L0 + wid*GK*64 + j*64 + lane) of the order that the
+// pass which wrote `src` defines, from that pass's digit totals (tot: thread tid < 256's
+// digit) and that buffer's tile rows (row t, digit d: local offset lo | count << 16).  In that order the runs (d, t) follow each other digit-major;
+// the tile overlaps the runs of the digits [dlo, dhi] whose logical range meets it.
+// Block-uniform (barriers).  Matches gs_gather on the tables k_gout would have written.
+__device__ __forceinline__ void gs_gather_f(const uint32_t *__restrict__ src, const uint32_t *__restrict__ rows,
+                                            uint32_t tot, uint32_t ntp, uint32_t n, uint32_t L0, uint32_t nvalid, uint32_t sentinel,
+                                            GsRunsF &g, uint32_t (&k)[GK], uint32_t tid, uint32_t lane,
+                                            uint32_t wid) {
+    if (tid < (uint32_t)(GT / 32)) g.bits[tid] = 0u;
+    if (tid == 0) {
+        g.dlo = 255u;
+        g.dhi = 0u;
+    }
+    __syncthreads();
+    const uint32_t L1 = L0 + nvalid;
+    const uint32_t gx = block_excl_scan<GB, 256>(tot, g.wsum);  // logical start of digit tid
+    const bool meets = tid < 256u && tot != 0u && gx < L1 && gx + tot > L0;
+    if (meets) {
+        atomicMin(&g.dlo, tid);
+        atomicMax(&g.dhi, tid);
+    }
+    __syncthreads();
+    if (meets && tid == g.dlo) g.base = gx;
+    __syncthreads();
+    const uint32_t dlo = g.dlo, E = g.dhi >= dlo ? (g.dhi - dlo + 1u) * ntp : 0u;  // runs (d, t), digit-major
+    const uint32_t base0 = g.base;
+    constexpr uint32_t C = 4, CH = GB * C;
+    // two sweeps over the runs: (0) mark the start of every nonempty run inside the tile,
+    // (1) store its delta (source address - logical position) at its rank among them.
+    // One chunk (the usual case: a tile meets ~3 digits): sweep 1 reuses sweep 0's loads.
+    const bool one = E <= CH;
+    uint32_t w[C], sr[C], ex1 = 0;
+#pragma unroll 1
+    for (int sweep = 0; sweep < 2; ++sweep) {
+        if (sweep == 1) {
+            const uint32_t pc = tid < (uint32_t)(GT / 32) ? (uint32_t)__popc(g.bits[tid]) : 0u;
+            const uint32_t ex = block_excl_scan<GB, GT / 32>(pc, g.wsum);
+            if (tid < (uint32_t)(GT / 32)) g.wpre[tid] = ex;
+            __syncthreads();
+        }
+        uint32_t base = base0;
+#pragma unroll 1
+        for (uint32_t c0 = 0; c0 < E; c0 += CH) {
+            uint32_t ex = ex1, chunk = 0;
+            if (!(one && sweep == 1)) {  // block-uniform
+                uint32_t s = 0;
+#pragma unroll
+                for (uint32_t j = 0; j < C; ++j) {
+                    const uint32_t e = c0 + tid * C + j;
+                    w[j] = 0u;
+                    sr[j] = 0u;
+                    if (e < E) {
+                        const uint32_t dd = dlo + e / ntp, t = e % ntp;
+                        w[j] = rows[(size_t)t * 256 + dd];
+                        sr[j] = t * (uint32_t)GT + (w[j] & 0xFFFFu);
+                    }
+                    s += w[j] >> 16;
+                }
+                ex = ex1 = block_excl_scan<GB, GB>(s, g.wsum);
+#pragma unroll
+                for (int q = 0; q < GB / 64; ++q) chunk += g.wsum[q];
+            }
+            uint32_t ls = base + ex;
+#pragma unroll
+            for (uint32_t j = 0; j < C; ++j) {
+                const uint32_t cnt = w[j] >> 16;
+                if (cnt != 0u && ls < L1 && ls + cnt > L0) {
+                    const uint32_t rel = ls > L0 ? ls - L0 : 0u, wd = rel >> 5, b = rel & 31u;
+                    if (sweep == 0) atomicOr(&g.bits[wd], 1u << b);
+                    else g.delta[g.wpre[wd] + (uint32_t)__popc(g.bits[wd] & ((1u << b) - 1u))] = (int32_t)(sr[j] - ls);
+                }
+                ls += cnt;
+            }
+            base += chunk;
+            __syncthreads();  // g.wsum reused by the next chunk's scan
+        }
+    }
+    const uint32_t pw = wid * (GK * WAVE) + lane;
+    uint32_t addr[GK];
+#pragma unroll
+    for (int j = 0; j < GK; ++j) {
+        const uint32_t p = pw + (uint32_t)j * WAVE;
+        const uint32_t w = (p >> 5) & (uint32_t)(GT / 32 - 1), b = p & 31u;
+        const uint32_t m = b == 31u ? 0xFFFFFFFFu : (2u << b) - 1u;
+        const uint32_t idx = g.wpre[w] + (uint32_t)__popc(g.bits[w] & m) - 1u;
+        const uint32_t a = L0 + p + (uint32_t)g.delta[idx < (uint32_t)GT ? idx : 0u];
+        addr[j] = a < n ? a : n - 1u;  // (never past the buffer, whatever the rows say)
+    }
+    if (nvalid == (uint32_t)GT) {
+#pragma unroll
+        for (int j = 0; j < GK; ++j) k[j] = ld_stream<NT_GS>(src + addr[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < GK; ++j) k[j] = pw + (uint32_t)j * WAVE < nvalid ? ld_stream<NT_GS>(src + addr[j]) : sentinel;
+    }
+}
+
 // LDS word of tile slot i in the reorder buffer: 4 pad words per 32 slots (16-B
 // aligned, for the uint4 write-out).  In a sorted tile every digit holds 32 keys, so a
 // wave's reorder stores land 32 slots apart: one bank unpadded, 8 banks padded.
@@ -184,7 +416,9 @@ struct GsSmem {
     union {  // the run tables are only read while the tile is gathered, before the reorder
         uint32_t keys[GT + GT / 8];
         GsRuns g;
+        GsRunsF f;  // fused small path
     };
+    uint32_t fpart[272];  // fused small path: gs_fused_prologue's scratch
     uint32_t wh[GW * 256];
     uint32_t probe[WAVE];
     uint32_t wsum[8];
@@ -194,16 +428,29 @@ struct GsSmem {
 
 // One pass: gather (or, for the input, load) tile T, sort it by digit `pass` in LDS,
 // write it contiguously to the other buffer, record its digit counts and offsets.
+// FUSED (small path): no scan launches; rt holds A's tile rows and rt2 B's, the tile's
+// runs come from gs_gather_f, the skip test from the tiles' digit min / max pairs.
+template <bool FUSED>
 __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *__restrict__ in, uint32_t *bufA, uint32_t *bufB,
                                                   GsTables tA, GsTables tB, uint32_t *__restrict__ rt,
-                                                  uint32_t *__restrict__ mm, GsState *st, int pass, uint32_t n,
-                                                  uint32_t ntp, uint32_t flip) {
-    if (!gs_active(st, pass)) return;
+                                                  uint32_t *__restrict__ rt2, uint32_t *__restrict__ mm, GsState *st,
+                                                  uint32_t *__restrict__ acc, int pass, uint32_t n, uint32_t ntp,
+                                                  uint32_t flip) {
+    if (!FUSED && !gs_active(st, pass)) return;
     const uint32_t T = gs_tile(blockIdx.x, ntp);
     if (T >= ntp) return;
     __shared__ GsSmem sm;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t cur = gs_cur(st, pass);
+    uint32_t ftot = 0;  // fused: this thread's digit total of the previous active pass
+    GsMM fmm;           // fused: digit min / max (pass > 0)
+    if (FUSED && pass > 0) {
+        ftot = gs_fused_prologue(acc, pass, fmm, sm.fpart, tid);
+        if (!gs_active(&fmm, pass)) {  // block-uniform
+            gs_forward(acc, pass, ftot, tid);
+            return;
+        }
+    }
+    const uint32_t cur = FUSED ? gs_cur(&fmm, pass) : gs_cur(st, pass);
     const uint32_t *src = cur == 0 ? in : cur == 1 ? bufA : bufB;
     uint32_t *dst = cur == 1 ? bufB : bufA;
     const uint32_t L0 = T * (uint32_t)GT;
@@ -229,7 +476,8 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
         }
         __syncthreads();
     } else {
-        gs_gather(src, cur == 1 ? tA : tB, T, L0, nvalid, sentinel, sm.g, k, tid, lane, wid);
+        if constexpr (FUSED) gs_gather_f(src, cur == 1 ? rt : rt2, ftot, ntp, n, L0, nvalid, sentinel, sm.f, k, tid, lane, wid);
+        else gs_gather(src, cur == 1 ? tA : tB, T, L0, nvalid, sentinel, sm.g, k, tid, lane, wid);
         __syncthreads();
     }
     const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
@@ -308,7 +556,8 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
             run += c;
         }
         const uint32_t cnt = tid == 255u ? tot - ((uint32_t)GT - nvalid) : tot;  // drop sentinels
-        rt[(size_t)T * 256 + tid] = ds | (cnt << 16);
+        (FUSED && dst == bufB ? rt2 : rt)[(size_t)T * 256 + tid] = ds | (cnt << 16);
+        if (FUSED && cnt) atomicAdd(acc + ((size_t)pass * GS_FSLOTS + T % GS_FSLOTS) * 256 + tid, cnt);  // next pass's totals
     }
     if (pass == 0 && tid == 0) {
         uint32_t mn = sm.mm[0][0], mx = sm.mm[0][1];
@@ -325,6 +574,14 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
         }
         mm[2 * T] = mn;
         mm[2 * T + 1] = mx;
+        if (FUSED) {
+            uint32_t *f = acc + GS_FACC_WORDS + (T % GS_FSLOTS) * 64u;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                atomicMax(f + q, 255u - ((mn >> (8 * q)) & 255u));
+                atomicMax(f + 4 + q, (mx >> (8 * q)) & 255u);
+            }
+        }
     }
     __syncthreads();  // (2) wave offsets
 
@@ -349,64 +606,6 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
             const uint32_t i = (uint32_t)j * GB + tid;
             if (i < nvalid) dst[L0 + i] = sm.keys[gs_pad(i)];
         }
-    }
-}
-
-// ---- scan of the tile rows ------------------------------------------------------------
-// bytewise min / max of packed digit words (byte q = digit q of key ^ flip)
-__device__ __forceinline__ uint32_t bmin4(uint32_t a, uint32_t b) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t x = (a >> (8 * q)) & 255u, y = (b >> (8 * q)) & 255u;
-        r |= (x < y ? x : y) << (8 * q);
-    }
-    return r;
-}
-__device__ __forceinline__ uint32_t bmax4(uint32_t a, uint32_t b) {
-    uint32_t r = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const uint32_t x = (a >> (8 * q)) & 255u, y = (b >> (8 * q)) & 255u;
-        r |= (x > y ? x : y) << (8 * q);
-    }
-    return r;
-}
-// Wave-wide bytewise min / max of (mn, mx) pairs, result in every lane.
-__device__ __forceinline__ void wave_minmax4(uint32_t &mn, uint32_t &mx) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        mn = bmin4(mn, __shfl_xor(mn, off));
-        mx = bmax4(mx, __shfl_xor(mx, off));
-    }
-}
-// Digit min / max over `cnt` packed (min, max) pairs into st->dmin / dmax.  Whole
-// block, block-uniform call (barrier).
-template <int BLOCK>
-__device__ __forceinline__ void gs_reduce_minmax(const uint32_t *pairs, uint32_t cnt, uint32_t (*red)[2],
-                                                 GsState *st) {
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    uint32_t mn = 0xFFFFFFFFu, mx = 0u;
-    for (uint32_t i = tid; i < cnt; i += BLOCK) {
-        mn = bmin4(mn, pairs[2 * i]);
-        mx = bmax4(mx, pairs[2 * i + 1]);
-    }
-    wave_minmax4(mn, mx);
-    if (lane == 0) {
-        red[wid][0] = mn;
-        red[wid][1] = mx;
-    }
-    __syncthreads();
-    if (tid < 4u) {
-        uint32_t a = 255u, b = 0u;
-#pragma unroll
-        for (int w = 0; w < BLOCK / WAVE; ++w) {
-            const uint32_t x = (red[w][0] >> (8 * tid)) & 255u, y = (red[w][1] >> (8 * tid)) & 255u;
-            a = x < a ? x : a;
-            b = y > b ? y : b;
-        }
-        st->dmin[tid] = a;
-        st->dmax[tid] = b;
     }
 }
 
@@ -559,18 +758,29 @@ __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, 
 }
 
 // Final pass: the logical order after the last pass, gathered and written to `out`.
+template <bool FUSED>
 __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gcopy(const uint32_t *__restrict__ bufA, const uint32_t *__restrict__ bufB,
-                                                 GsTables tA, GsTables tB, const GsState *st,
-                                                 uint32_t *__restrict__ out, uint32_t n, uint32_t ntp) {
+                                                 GsTables tA, GsTables tB, const uint32_t *__restrict__ rt,
+                                                 const uint32_t *__restrict__ rt2, const GsState *st,
+                                                 const uint32_t *__restrict__ acc, uint32_t *__restrict__ out, uint32_t n,
+                                                 uint32_t ntp) {
     const uint32_t T = gs_tile(blockIdx.x, ntp);
     if (T >= ntp) return;
-    __shared__ GsRuns g;
+    __shared__ union {
+        GsRuns g;
+        GsRunsF f;
+    } u;
+    __shared__ uint32_t fpart[272];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t cur = gs_cur(st, 4);
+    uint32_t ftot = 0;
+    GsMM fmm;
+    if constexpr (FUSED) ftot = gs_fused_prologue(acc, 4, fmm, fpart, tid);
+    const uint32_t cur = FUSED ? gs_cur(&fmm, 4) : gs_cur(st, 4);
     const uint32_t L0 = T * (uint32_t)GT;
     const uint32_t nvalid = (n - L0) < (uint32_t)GT ? (n - L0) : (uint32_t)GT;
     uint32_t k[GK];
-    gs_gather(cur == 1 ? bufA : bufB, cur == 1 ? tA : tB, T, L0, nvalid, 0u, g, k, tid, lane, wid);
+    if constexpr (FUSED) gs_gather_f(cur == 1 ? bufA : bufB, cur == 1 ? rt : rt2, ftot, ntp, n, L0, nvalid, 0u, u.f, k, tid, lane, wid);
+    else gs_gather(cur == 1 ? bufA : bufB, cur == 1 ? tA : tB, T, L0, nvalid, 0u, u.g, k, tid, lane, wid);
     uint32_t *o = out + L0 + wid * (GK * WAVE) + lane;
     const uint32_t woff = wid * (GK * WAVE) + lane;
 #pragma unroll
@@ -580,6 +790,12 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gcopy(const uint32_t *_
 
 inline size_t al(size_t x) { return (x + 65535) / 65536 * 65536; }
 
+// LABSORT_GS_FUSED=0 keeps the scan launches at every size (A/B)
+bool gs_fused(uint32_t ng) {
+    const char *e = std::getenv("LABSORT_GS_FUSED");
+    return ng <= (uint32_t)GS_SMALL_NG && !(e && e[0] == '0');
+}
+
 }  // namespace
 
 // ---- host side -------------------------------------------------------------------------
@@ -587,14 +803,18 @@ GsLayout gs_layout(size_t n) {
     GsLayout L{};
     const size_t ntp = (n + GT - 1) / GT, ng = (ntp + GS_GROUP - 1) / GS_GROUP, ne = 256 * ntp;
     size_t o = 0;
-    L.off_state = o;  // state, then the scan look-back flags of the 4 passes: zeroed together
-    o = al(o + 512 + 4 * ng * 256 * 4);
+    // state, then the scan look-back flags of the 4 passes, or (fused small path) the 4 x
+    // GS_FSLOTS copies of the digit totals: zeroed together
+    L.off_state = o;
+    o = al(o + 512 + std::max<size_t>(4 * ng * 256 * 4, ng <= (size_t)GS_SMALL_NG ? GS_FWORDS * 4 : 0));
     L.off_a = o;
     o = al(o + n * 4);
     L.off_b = o;
     o = al(o + n * 4);
     L.off_rt = o;
     o = al(o + ne * 4);
+    L.off_rt2 = o;  // B's tile rows (fused small path only)
+    if (ng <= (size_t)GS_SMALL_NG) o = al(o + ne * 4);
     L.off_mm = o;
     o = al(o + ntp * 8);
     L.off_gsx = o;
@@ -629,12 +849,28 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
         t[i] = GsTables{reinterpret_cast<uint32_t *>(ws + L.off_ls[i]), reinterpret_cast<uint32_t *>(ws + L.off_sr[i]),
                         reinterpret_cast<uint32_t *>(ws + L.off_first[i])};
     uint32_t *flags = reinterpret_cast<uint32_t *>(ws + L.off_state + 512);
-    hipError_t e = launch_zero(ws + L.off_state, 512 + (ng > (uint32_t)GS_SMALL_NG ? (size_t)4 * ng * 256 * 4 : 0), s);
-    if (e != hipSuccess) return e;
+    uint32_t *rt2 = reinterpret_cast<uint32_t *>(ws + L.off_rt2);
     const unsigned grid = 8u * ((ntp + 7u) / 8u);
+    hipError_t e;
+    if (gs_fused(ng)) {  // six launches: header memset, sweeps 0-3, the gathered copy
+        uint32_t *acc = flags;
+        if ((e = launch_zero(ws + L.off_state, 512 + GS_FWORDS * 4, s)) != hipSuccess) return e;
+        for (int p = 0; p < 4; ++p) {
+            if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GSWEEP, s);
+            k_gsweep<true><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, acc, p, (uint32_t)n, ntp, flip);
+            if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+        }
+        if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GCOPY, s);
+        k_gcopy<true><<<grid, GB, 0, s>>>(A, B, t[0], t[1], rt, rt2, st, acc, out, (uint32_t)n, ntp);
+        if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GCOPY, s);
+        return hipGetLastError();
+    }
+    e = launch_zero(ws + L.off_state, 512 + (ng > (uint32_t)GS_SMALL_NG ? (size_t)4 * ng * 256 * 4 : 0), s);
+    if (e != hipSuccess) return e;
     for (int p = 0; p < 4; ++p) {
         if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GSWEEP, s);
-        k_gsweep<<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, mm, st, p, (uint32_t)n, ntp, flip);
+        k_gsweep<false><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, flags, p, (uint32_t)n, ntp, flip);
         if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (ng <= (uint32_t)GS_SMALL_NG) {
@@ -647,7 +883,7 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GCOPY, s);
-    k_gcopy<<<grid, GB, 0, s>>>(A, B, t[0], t[1], st, out, (uint32_t)n, ntp);
+    k_gcopy<false><<<grid, GB, 0, s>>>(A, B, t[0], t[1], rt, rt2, st, flags, out, (uint32_t)n, ntp);
     if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GCOPY, s);
     return hipGetLastError();
 }
