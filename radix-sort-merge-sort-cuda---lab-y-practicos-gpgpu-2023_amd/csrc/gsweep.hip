@@ -303,6 +303,28 @@ __device__ __forceinline__ uint32_t gs_fused_prologue(const uint32_t *acc, int p
     return h ? 0u : c + part[d];
 }
 
+// Pass 1 when no memset ran (LABSORT_GS_FUSED=2): pass 0 accumulated nothing, so the
+// digit min / max come from its per-tile pairs and the totals from its 128 tile rows
+// (every workgroup sums them: 128 KB from L2), and workgroup 0 publishes the min / max
+// in line 0 of the min / max lines for the passes after it.  part: 288 words.
+__device__ __forceinline__ uint32_t gs_fused_prologue1(const uint32_t *rows, const uint32_t *mmp, uint32_t ntp,
+                                                       uint32_t *acc, GsMM &mm, uint32_t *part, uint32_t tid) {
+    const uint32_t d = tid & 255u, h = tid >> 8;
+    uint32_t c = 0;
+#pragma unroll 8
+    for (uint32_t t = h; t < ntp; t += 2u) c += rows[(size_t)t * 256 + d] >> 16;
+    GsMM *lmm = reinterpret_cast<GsMM *>(part + 256);
+    gs_reduce_minmax<GB>(mmp, ntp, reinterpret_cast<uint32_t (*)[2]>(part + 264), lmm);
+    if (h) part[d] = c;
+    __syncthreads();
+    mm = *lmm;
+    if (blockIdx.x == 0 && tid < 4u) {
+        acc[GS_FACC_WORDS + tid] = 255u - mm.dmin[tid];
+        acc[GS_FACC_WORDS + 4u + tid] = mm.dmax[tid];
+    }
+    return h ? 0u : c + part[d];
+}
+
 // A skipped pass p: workgroup 0 forwards the totals it received to acc[p] (copy 0; the
 // other copies stay zero), where pass p + 1 (or the final copy) reads them.
 __device__ __forceinline__ void gs_forward(uint32_t *acc, int p, uint32_t tot, uint32_t tid) {
@@ -418,7 +440,7 @@ struct GsSmem {
         GsRuns g;
         GsRunsF f;  // fused small path
     };
-    uint32_t fpart[272];  // fused small path: gs_fused_prologue's scratch
+    uint32_t fpart[288];  // fused small path: the prologues' scratch
     uint32_t wh[GW * 256];
     uint32_t probe[WAVE];
     uint32_t wsum[8];
@@ -435,7 +457,7 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
                                                   GsTables tA, GsTables tB, uint32_t *__restrict__ rt,
                                                   uint32_t *__restrict__ rt2, uint32_t *__restrict__ mm, GsState *st,
                                                   uint32_t *__restrict__ acc, int pass, uint32_t n, uint32_t ntp,
-                                                  uint32_t flip) {
+                                                  uint32_t flip, int nozero) {
     if (!FUSED && !gs_active(st, pass)) return;
     const uint32_t T = gs_tile(blockIdx.x, ntp);
     if (T >= ntp) return;
@@ -444,13 +466,19 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
     uint32_t ftot = 0;  // fused: this thread's digit total of the previous active pass
     GsMM fmm;           // fused: digit min / max (pass > 0)
     if (FUSED && pass > 0) {
-        ftot = gs_fused_prologue(acc, pass, fmm, sm.fpart, tid);
+        ftot = (nozero && pass == 1) ? gs_fused_prologue1(rt, mm, ntp, acc, fmm, sm.fpart, tid)
+                                     : gs_fused_prologue(acc, pass, fmm, sm.fpart, tid);
         if (!gs_active(&fmm, pass)) {  // block-uniform
             gs_forward(acc, pass, ftot, tid);
             return;
         }
     }
     const uint32_t cur = FUSED ? gs_cur(&fmm, pass) : gs_cur(st, pass);
+    if (FUSED && nozero && pass == 0 && T == 0) {  // what the memset would have cleared
+        if (tid == 0) st->err = 0u;
+        uint4 *z = reinterpret_cast<uint4 *>(acc + (size_t)GS_FSLOTS * 256);  // acc[1..3], min / max lines
+        for (uint32_t i = tid; i < (uint32_t)((GS_FWORDS - GS_FSLOTS * 256) / 4); i += GB) z[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
     const uint32_t *src = cur == 0 ? in : cur == 1 ? bufA : bufB;
     uint32_t *dst = cur == 1 ? bufB : bufA;
     const uint32_t L0 = T * (uint32_t)GT;
@@ -557,7 +585,8 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
         }
         const uint32_t cnt = tid == 255u ? tot - ((uint32_t)GT - nvalid) : tot;  // drop sentinels
         (FUSED && dst == bufB ? rt2 : rt)[(size_t)T * 256 + tid] = ds | (cnt << 16);
-        if (FUSED && cnt) atomicAdd(acc + ((size_t)pass * GS_FSLOTS + T % GS_FSLOTS) * 256 + tid, cnt);  // next pass's totals
+        if (FUSED && cnt && !(nozero && pass == 0))
+            atomicAdd(acc + ((size_t)pass * GS_FSLOTS + T % GS_FSLOTS) * 256 + tid, cnt);  // next pass's totals
     }
     if (pass == 0 && tid == 0) {
         uint32_t mn = sm.mm[0][0], mx = sm.mm[0][1];
@@ -574,7 +603,7 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gsweep(const uint32_t *
         }
         mm[2 * T] = mn;
         mm[2 * T + 1] = mx;
-        if (FUSED) {
+        if (FUSED && !nozero) {
             uint32_t *f = acc + GS_FACC_WORDS + (T % GS_FSLOTS) * 64u;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -790,10 +819,13 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gcopy(const uint32_t *_
 
 inline size_t al(size_t x) { return (x + 65535) / 65536 * 65536; }
 
-// LABSORT_GS_FUSED=0 keeps the scan launches at every size (A/B)
-bool gs_fused(uint32_t ng) {
+// LABSORT_GS_FUSED: 0 keeps the scan launches at every size (A/B); 1 clears the
+// accumulators with a memset launch; 2 has pass 0 clear those of passes 1-3 and pass 1
+// read pass 0's rows and pairs
+int gs_fused(uint32_t ng) {
     const char *e = std::getenv("LABSORT_GS_FUSED");
-    return ng <= (uint32_t)GS_SMALL_NG && !(e && e[0] == '0');
+    if (ng > (uint32_t)GS_SMALL_NG || (e && e[0] == '0')) return 0;
+    return (e && e[0] == '1') ? 1 : 2;
 }
 
 }  // namespace
@@ -852,12 +884,13 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
     uint32_t *rt2 = reinterpret_cast<uint32_t *>(ws + L.off_rt2);
     const unsigned grid = 8u * ((ntp + 7u) / 8u);
     hipError_t e;
-    if (gs_fused(ng)) {  // six launches: header memset, sweeps 0-3, the gathered copy
+    if (const int fz = gs_fused(ng)) {  // sweeps 0-3, the gathered copy (+ a memset: fz = 1)
         uint32_t *acc = flags;
-        if ((e = launch_zero(ws + L.off_state, 512 + GS_FWORDS * 4, s)) != hipSuccess) return e;
+        if (fz == 1 && (e = launch_zero(ws + L.off_state, 512 + GS_FWORDS * 4, s)) != hipSuccess) return e;
         for (int p = 0; p < 4; ++p) {
             if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GSWEEP, s);
-            k_gsweep<true><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, acc, p, (uint32_t)n, ntp, flip);
+            k_gsweep<true><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, acc, p, (uint32_t)n, ntp, flip,
+                                               fz == 2);
             if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
@@ -870,7 +903,7 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
     if (e != hipSuccess) return e;
     for (int p = 0; p < 4; ++p) {
         if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GSWEEP, s);
-        k_gsweep<false><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, flags, p, (uint32_t)n, ntp, flip);
+        k_gsweep<false><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, flags, p, (uint32_t)n, ntp, flip, 0);
         if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (ng <= (uint32_t)GS_SMALL_NG) {
