@@ -715,6 +715,22 @@ def main():
     # the host-pointer leg runs once every rank is done with its GPU
     hostp = host_leg(args) if rank == 0 and not args.no_host_path and args.backend == "nccl" else None
 
+    # the measured copy ceiling: a device-to-device copy of the same n keys (torch copy_,
+    # i.e. hipMemcpy D2D), the practical HBM rate a read-once write-once pass can reach
+    copy_gbs = None
+    if rank == 0 and world == 1:
+        cp = torch.empty_like(src)
+        for _ in range(3):
+            cp.copy_(src)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            cp.copy_(src)
+        e1.record()
+        e1.synchronize()
+        copy_gbs = 8.0 * n * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        del cp
+
     if rank == 0:
         avg_ms = k_ms / k_cnt if k_cnt else None
         per_launch_bytes = 16.0 * n if args.algo == "pairs" else 8.0 * n  # key (+ payload) read + written
@@ -727,6 +743,10 @@ def main():
                                "k_onesweep<8, KV>" if args.algo == "pairs" and dom == "onesweep" else f"k_{dom}"), "launches": k_cnt,
                     "avg_launch_ms": round(avg_ms, 5) if avg_ms else None,
                     "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
+        if copy_gbs and achieved:
+            roofline["copy_ceiling"] = {"value": round(copy_gbs, 1), "unit": "GB/s", "frac": round(achieved / copy_gbs, 4),
+                                        "probe": "device-to-device copy of the same n keys (torch copy_ = hipMemcpy "
+                                                 "D2D, 10 runs, read + write bytes), same box, after the timed region"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(args.cpu_seconds, n, ls)
@@ -756,6 +776,11 @@ def main():
                 "; payloads gather the output keys, stable" if args.algo == "pairs" and world == 1 else ""),
             "roofline": roofline, "cpu_baseline": cpu,
         }
+        if copy_gbs:  # each leg's dominant kernel against the same measured copy rate
+            for leg in (merge_leg and merge_leg["roofline"], merge_leg and merge_leg["tile_sort"],
+                        pairs_leg and pairs_leg["roofline"]):
+                if leg and leg.get("achieved"):
+                    leg["copy_frac"] = round(leg["achieved"] / copy_gbs, 4)
         if merge_leg:
             line["merge"] = merge_leg
         if config1:
