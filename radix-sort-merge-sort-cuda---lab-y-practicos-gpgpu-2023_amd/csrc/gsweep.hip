@@ -257,8 +257,8 @@ struct GsRunsF {
     uint32_t bits[GT / 32];
     uint32_t wpre[GT / 32];
     int32_t delta[GT];
+    uint32_t tot[256];  // digit totals of the logical order
     uint32_t wsum[8];
-    uint32_t dlo, dhi, base;
 };
 
 // Fused small path: each active pass q adds its tiles' digit counts into acc[q], spread
@@ -340,24 +340,107 @@ __device__ __forceinline__ void gs_gather_f(const uint32_t *__restrict__ src, co
                                             uint32_t tot, uint32_t ntp, uint32_t n, uint32_t L0, uint32_t nvalid, uint32_t sentinel,
                                             GsRunsF &g, uint32_t (&k)[GK], uint32_t tid, uint32_t lane,
                                             uint32_t wid) {
+    // the digit totals to LDS; every wave then scans them itself (4 digits per lane) for
+    // the digits [dlo, dhi] whose logical range meets the tile and the logical start of
+    // dlo: no block scan, no barrier
+    if (tid < 256u) g.tot[tid] = tot;
     if (tid < (uint32_t)(GT / 32)) g.bits[tid] = 0u;
-    if (tid == 0) {
-        g.dlo = 255u;
-        g.dhi = 0u;
-    }
     __syncthreads();
     const uint32_t L1 = L0 + nvalid;
-    const uint32_t gx = block_excl_scan<GB, 256>(tot, g.wsum);  // logical start of digit tid
-    const bool meets = tid < 256u && tot != 0u && gx < L1 && gx + tot > L0;
-    if (meets) {
-        atomicMin(&g.dlo, tid);
-        atomicMax(&g.dhi, tid);
+    uint32_t dlo = 1, dhi = 0, base0 = 0;
+    {
+        const uint4 t4 = *reinterpret_cast<const uint4 *>(&g.tot[4u * lane]);
+        const uint32_t tv[4] = {t4.x, t4.y, t4.z, t4.w};
+        const uint32_t sum = t4.x + t4.y + t4.z + t4.w;
+        uint32_t x = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(x, off);
+            if (lane >= (uint32_t)off) x += y;
+        }
+        uint32_t gd = x - sum, first = 4u, last = 0u, gfirst = 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            if (tv[q] != 0u && gd < L1 && gd + tv[q] > L0) {
+                if (first == 4u) {
+                    first = q;
+                    gfirst = gd;
+                }
+                last = q;
+            }
+            gd += tv[q];
+        }
+        const uint64_t b = __ballot(first != 4u);
+        if (b) {
+            const int fl = __builtin_ctzll(b), ll = 63 - __builtin_clzll(b);
+            dlo = 4u * (uint32_t)fl + (uint32_t)__shfl((int)first, fl);
+            dhi = 4u * (uint32_t)ll + (uint32_t)__shfl((int)last, ll);
+            base0 = (uint32_t)__shfl((int)gfirst, fl);
+        }
     }
-    __syncthreads();
-    if (meets && tid == g.dlo) g.base = gx;
-    __syncthreads();
-    const uint32_t dlo = g.dlo, E = g.dhi >= dlo ? (g.dhi - dlo + 1u) * ntp : 0u;  // runs (d, t), digit-major
-    const uint32_t base0 = g.base;
+    const uint32_t E = dhi >= dlo ? (dhi - dlo + 1u) * ntp : 0u;  // runs (d, t), digit-major
+    constexpr uint32_t CW = 8;  // runs per lane of the one-wave path
+    if (E <= WAVE * CW) {  // block-uniform: the usual case (a tile meets ~3 digits), wave 0 alone
+        if (wid == 0) {
+            uint32_t w[CW], sr[CW], s = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < CW; ++j) {
+                const uint32_t e = lane * CW + j;
+                w[j] = 0u;
+                sr[j] = 0u;
+                if (e < E) {
+                    const uint32_t dd = dlo + e / ntp, t = e % ntp;
+                    w[j] = rows[(size_t)t * 256 + dd];
+                    sr[j] = t * (uint32_t)GT + (w[j] & 0xFFFFu);
+                }
+                s += w[j] >> 16;
+            }
+            uint32_t x = s;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(x, off);
+                if (lane >= (uint32_t)off) x += y;
+            }
+            const uint32_t ls0 = base0 + x - s;
+            uint32_t ls = ls0;
+#pragma unroll
+            for (uint32_t j = 0; j < CW; ++j) {
+                const uint32_t cnt = w[j] >> 16;
+                if (cnt != 0u && ls < L1 && ls + cnt > L0) {
+                    const uint32_t rel = ls > L0 ? ls - L0 : 0u;
+                    atomicOr(&g.bits[rel >> 5], 1u << (rel & 31u));
+                }
+                ls += cnt;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            // popcount prefix of the 256 bitmap words, 4 per lane
+            const uint4 b4 = *reinterpret_cast<const uint4 *>(&g.bits[4u * lane]);
+            const uint32_t p0 = (uint32_t)__popc(b4.x), p1 = (uint32_t)__popc(b4.y), p2 = (uint32_t)__popc(b4.z),
+                           p3 = (uint32_t)__popc(b4.w), ps = p0 + p1 + p2 + p3;
+            uint32_t y = ps;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t z = __shfl_up(y, off);
+                if (lane >= (uint32_t)off) y += z;
+            }
+            const uint32_t e0 = y - ps;
+            *reinterpret_cast<uint4 *>(&g.wpre[4u * lane]) = make_uint4(e0, e0 + p0, e0 + p0 + p1, e0 + p0 + p1 + p2);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            ls = ls0;
+#pragma unroll
+            for (uint32_t j = 0; j < CW; ++j) {
+                const uint32_t cnt = w[j] >> 16;
+                if (cnt != 0u && ls < L1 && ls + cnt > L0) {
+                    const uint32_t rel = ls > L0 ? ls - L0 : 0u, wd = rel >> 5, bb = rel & 31u;
+                    g.delta[g.wpre[wd] + (uint32_t)__popc(g.bits[wd] & ((1u << bb) - 1u))] = (int32_t)(sr[j] - ls);
+                }
+                ls += cnt;
+            }
+        }
+        __syncthreads();
+    } else {
     constexpr uint32_t C = 4, CH = GB * C;
     // two sweeps over the runs: (0) mark the start of every nonempty run inside the tile,
     // (1) store its delta (source address - logical position) at its rank among them.
@@ -409,6 +492,7 @@ __device__ __forceinline__ void gs_gather_f(const uint32_t *__restrict__ src, co
             __syncthreads();  // g.wsum reused by the next chunk's scan
         }
     }
+    }  // (many runs: the whole block, in chunks)
     const uint32_t pw = wid * (GK * WAVE) + lane;
     uint32_t addr[GK];
 #pragma unroll
