@@ -211,8 +211,9 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
             HIP_TRY(launch_hist_seg(in, n, flip, hps, joint, s));
         }
-        HIP_TRY(launch_zero(ws + L.off_lookback, L.zero_bytes - L.off_lookback, s));
-        HIP_TRY(launch_plan8(hps, joint, n, in == out ? 1 : 0, plan, sps, hist, s));
+        // the look-back clear rides in the plan launch (k_plan8's workgroups 1..)
+        HIP_TRY(launch_plan8(hps, joint, n, in == out ? 1 : 0, plan, sps, hist, ws + L.off_lookback,
+                             L.zero_bytes - L.off_lookback, s));
         for (int p = 0; p < L.P; ++p) {
             TimingScope ts(LABSORT_K_ONESWEEP, s);
             // (LABSORT_OSP_JCOUNT timing builds count into hps, free once the plan is built)
@@ -779,8 +780,8 @@ int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint3
             TimingScope ts(LABSORT_K_HISTOGRAM, s);
             HIP_TRY(launch_hist_seg(ki, n, flip, hps, joint, s));
         }
-        HIP_TRY(launch_zero(ws + L.off_lookback, L.zero_bytes - L.off_lookback, s));
-        HIP_TRY(launch_plan8(hps, joint, n, ki == ko ? 1 : 0, plan, sps, hist, s));
+        HIP_TRY(launch_plan8(hps, joint, n, ki == ko ? 1 : 0, plan, sps, hist, ws + L.off_lookback,
+                             L.zero_bytes - L.off_lookback, s));
         for (int p = 0; p < L.P; ++p) {
             TimingScope ts(LABSORT_K_ONESWEEP, s);
             HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,

@@ -296,7 +296,7 @@ hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t 
 hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, uint32_t *joint,
                            hipStream_t s);
 hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, int in_is_out, Plan *plan,
-                        SegPlan *segplans, uint32_t *hist, hipStream_t s);
+                        SegPlan *segplans, uint32_t *hist, void *zero_p, size_t zero_bytes, hipStream_t s);
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
                              uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s,
                              const Bufs *vb = nullptr, uint32_t *jout = nullptr);

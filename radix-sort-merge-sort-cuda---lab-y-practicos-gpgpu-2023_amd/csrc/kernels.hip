@@ -402,9 +402,19 @@ __device__ void build_segplan_later(SegPlan *__restrict__ sps, int q, uint32_t p
 // buffers; plus each pass's next active digit) and every active pass's SegPlan (the
 // later passes' plans depend only on the histograms, so they are built here, not by
 // a launch before each pass).
+// Workgroups 1.. clear the look-back region (zp, zn4 uint4s) while workgroup 0 builds the
+// plans: one launch instead of a k_zero launch and this one (the look-back words are
+// only read by the passes after it).
 __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps, const uint32_t *__restrict__ joint,
                                                uint32_t n, int in_is_out, int seg_later, Plan *__restrict__ plan,
-                                               SegPlan *__restrict__ sps, uint32_t *__restrict__ hist_out) {
+                                               SegPlan *__restrict__ sps, uint32_t *__restrict__ hist_out,
+                                               uint4 *__restrict__ zp, size_t zn4) {
+    if (blockIdx.x > 0) {
+        const size_t stride = (size_t)(gridDim.x - 1) * blockDim.x;
+        for (size_t i = (size_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < zn4; i += stride)
+            zp[i] = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
     __shared__ uint32_t hist[4 * 256];
     __shared__ uint32_t sh[NSEG * 256 + 8];
     __shared__ uint32_t triv[4];
@@ -1425,6 +1435,13 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
             if (c) atomicAdd(jout + i, c);
         }
     }
+#ifndef LABSORT_OSP_TAILWB
+#define LABSORT_OSP_TAILWB 0
+#endif
+    // LABSORT_OSP_TAILWB (experiment): a workgroup out of tiles releases at agent scope,
+    // so its XCD's L2 starts writing back dirty lines while other workgroups still run,
+    // instead of all of it at the kernel-end release (the ~10 us between passes)
+    if constexpr (LABSORT_OSP_TAILWB != 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
 #ifdef OSP_STAMPS
     if (lane == 0)
         for (int i = 0; i < 10; ++i) atomicAdd(&g_osp_stamps[i], st_[i]);
@@ -2240,8 +2257,18 @@ static int seg_later() {
 }
 
 hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, int in_is_out, Plan *plan,
-                        SegPlan *segplans, uint32_t *hist, hipStream_t s) {
-    k_plan8<<<1, 256, 0, s>>>(hps, joint, (uint32_t)n, in_is_out, seg_later(), plan, segplans, hist);
+                        SegPlan *segplans, uint32_t *hist, void *zero_p, size_t zero_bytes, hipStream_t s) {
+    // LABSORT_PLAN_ZERO=0: the look-back clear as its own k_zero launch (A/B)
+    const char *e = std::getenv("LABSORT_PLAN_ZERO");
+    const bool fold = !(e && e[0] == '0') && zero_bytes % 16 == 0;
+    if (!fold && zero_bytes) {
+        const hipError_t z = launch_zero(zero_p, zero_bytes, s);
+        if (z != hipSuccess) return z;
+    }
+    const size_t zn4 = fold ? zero_bytes / 16 : 0;
+    const unsigned g = 1u + (zn4 ? blocks_for(zn4, 256 * 4, 2048) : 0u);
+    k_plan8<<<g, 256, 0, s>>>(hps, joint, (uint32_t)n, in_is_out, seg_later(), plan, segplans, hist,
+                              static_cast<uint4 *>(zero_p), zn4);
     return hipGetLastError();
 }
 
