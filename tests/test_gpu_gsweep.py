@@ -157,3 +157,16 @@ def test_gather_fused_repeat_same_workspace(ls, oracle, torch_gpu, monkeypatch, 
         ls.sort_device(t, o, n, key="u32", algo="radix", workspace=ws)
         ls.workspace_status(ws, n, "radix")
         np.testing.assert_array_equal(from_dev(o), oracle.sort_u32(a))
+
+
+@pytest.mark.parametrize("plan_zero", ["1", "0"])
+@pytest.mark.parametrize("inplace", [False, True])
+def test_onesweep_lookback_clear(ls, oracle, torch_gpu, monkeypatch, plan_zero, inplace):
+    """the look-back clear folded into the plan launch (default) or as its own k_zero
+    (LABSORT_PLAN_ZERO=0); a dirty workspace from the previous sort must not leak"""
+    monkeypatch.setenv("LABSORT_PLAN_ZERO", plan_zero)
+    n = (1 << 22) + 4097
+    for i in range(2):
+        a = oracle.gen(n, SEED + 50 + i, "u32")
+        np.testing.assert_array_equal(sort_impl(ls, torch_gpu, a, "u32", "onesweep", monkeypatch, inplace),
+                                      oracle.sort_u32(a))
