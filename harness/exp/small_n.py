@@ -39,4 +39,12 @@ for n in [int(x) for x in os.environ.get("NS", "").split()] or [256, 4096, 32768
         ls.workspace_status(ws, n, algo)
         assert torch.equal(o, ref), (n, name)
         row[name + "_ms"] = round(ts[len(ts) // 2], 4)
+        if os.environ.get("B2B"):  # also 50 sorts back to back (bench.py's config-2 timing)
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for _ in range(50):
+                ls.sort_device(d, o, n, algo=algo, workspace=ws)
+            b.record()
+            b.synchronize()
+            row[name + "_b2b_ms"] = round(a.elapsed_time(b) / 50, 4)
     print(json.dumps(row), flush=True)
