@@ -7,7 +7,7 @@
  *
  *   order_array      lab.h:9  / lab.cu:303  sort `length` ints in place (host
  *                    pointer, synchronous) on the MI355X; default algorithm
- *                    LABSORT_ALGO_AUTO (merge path up to 2^18 keys and past the
+ *                    LABSORT_ALGO_AUTO (merge path up to 2^16 keys and past the
  *                    radix limit, LSD radix between); LABSORT_ALGO=radix|merge|radix1
  *                    selects one; LABSORT_GPUS=p sorts across devices 0..p-1.
  *   order_with_trust lab.h:10 / lab.cu:404  thrust::sort on the host pointer

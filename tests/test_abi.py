@@ -84,12 +84,12 @@ def test_sizes_and_limits(ls):
             prev = w
             if n > TS:
                 assert w >= 4 * n  # one ping-pong buffer of n keys
-    # auto (the drop-ins' default): merge up to 2^18 keys, radix above, merge again past
+    # auto (the drop-ins' default): merge up to 2^16 keys, radix above, merge again past
     # the radix limit (the reference's 2^30-key config)
     assert ls.max_keys("auto") == ls.max_keys("merge")
-    for n in (1, TS + 1, 1 << 17, 1 << 18, 1 << 30, (1 << 30) + 7):
+    for n in (1, TS + 1, 1 << 16, 1 << 30, (1 << 30) + 7):
         assert ls.workspace_bytes(n, "auto") == ls.workspace_bytes(n, "merge")
-    for n in ((1 << 18) + 1, 1 << 20, 1 << 22, 1 << 28, (1 << 30) - 1):
+    for n in ((1 << 16) + 1, 1 << 17, 1 << 18, 1 << 20, 1 << 22, 1 << 28, (1 << 30) - 1):
         assert ls.workspace_bytes(n, "auto") == ls.workspace_bytes(n, "radix")
     # radix is sized for the implementation that runs: at 2^28 the onesweep
     # passes' ping-pong keys + 4 passes of look-back words (one slot of 256 digits per
