@@ -9,14 +9,17 @@ copies, lab.cu:321-397).  Keys are generated on the device (counter-based
 generator, seed 0x5EED0003) and stay resident in HBM; the sort is out of place
 so every step sorts the same input.
 
-N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): the
-merge-sort path of the north_star through the product's C-ABI: every rank calls
-labsort_dist_sort on its communicator (labsort_comm_init_rccl, rank 0's unique id
-broadcast over torch.distributed).  Each rank holds a fixed 2^log2n-key shard (weak
-scaling), sorts it locally with the radix kernels, then the splitter exchange moves
-keys by grouped ncclSend/ncclRecv and each rank merges its received runs
-(csrc/dist_plan.h).  --exchange pairwise runs the Python bitonic merge-split network
-(dist.py) instead.  value = all ranks' keys / max-over-ranks time.
+N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): BASELINE config 5,
+the merge-sort path of the north_star through the product's C-ABI: a 2^30-key array
+(--total-log2n) partitioned over the N ranks (2^30/N keys each: strong scaling); every
+rank calls labsort_dist_sort on its communicator (labsort_comm_init_rccl, rank 0's unique
+id broadcast over torch.distributed), which sorts its shard locally with the radix
+kernels, moves keys by grouped ncclSend/ncclRecv at the splitters and merges its received
+runs (csrc/dist_plan.h).  value = all ranks' keys / max-over-ranks time.  The same
+schedule with 2^log2n keys per rank (weak scaling) is reported beside it ("weak").
+--exchange pairwise runs the Python bitonic merge-split network (dist.py) instead;
+--backend gloo runs the schedule over host collectives (several ranks on one GPU: a
+rehearsal, not a measurement of xGMI).
 
 host_path (after the timed region, rank 0, in a child process): the reference's
 own calling convention -- a pageable host int* of 2^30 keys (BASELINE config 5)
@@ -59,7 +62,10 @@ def parse():
     ap.add_argument("--algo", default="radix", choices=["radix", "merge", "radix1", "pairs"],
                     help="pairs: stable key/value sort (sort_by_key) of (key, uint32 index) pairs")
     ap.add_argument("--pair-algo", default="radix", choices=["radix", "merge"], help="--algo pairs: which path")
-    ap.add_argument("--log2n", type=int, default=28, help="keys per GPU = 2^log2n")
+    ap.add_argument("--log2n", type=int, default=28, help="N = 1: keys = 2^log2n; N > 1: keys per GPU of the weak-scaling field")
+    ap.add_argument("--total-log2n", type=int, default=30,
+                    help="N > 1: the whole array (BASELINE config 5: 2^30 keys) partitioned over the N ranks")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling (2^log2n per GPU) field")
     ap.add_argument("--dist", default="u32")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-merge", action="store_true", help="skip the merge-sort leg (config 4) of the N=1 radix run")
@@ -375,6 +381,173 @@ def host_leg(args, timeout_s: int = 100):
     return out
 
 
+def dist_leg(torch, ls, dmod, args, dev, cdev, stream, rank, world, sizes, seed, dcomm=None, comm=None):
+    """One N > 1 measurement: rank r sorts its shard of sizes[r] keys (keys first ..
+    first + sizes[r] of the generator: the shards are the global array's pieces) as one
+    step of the distributed merge sort, W untimed + K timed steps between barriers, the
+    max over ranks of the elapsed time; then the global result is verified (every range
+    sorted, ranges in rank order, the same digit histograms and sum as the input)."""
+    import torch.distributed as dist
+    key = "u32"
+    m, first = sizes[rank], sum(sizes[:rank])
+    src = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+    if m:
+        ls.fill(src, m, SEED + 5, args.dist, first=first, stream=stream)
+    torch.cuda.synchronize()
+    if args.exchange == "splitters":
+        def step():  # the product: labsort_dist_sort (csrc/dist_plan.h's schedule)
+            ptr, cnt, _ = dcomm.sort(src, m, key=key, stream=stream)
+            return ptr, cnt
+    else:
+        ops = dmod.HipOps(ls, key=key, local_algo="radix", stream=stream)
+
+        def step():
+            with torch.cuda.stream(stream):
+                return dmod.dist_sort(src[:m], ops, copy_input=True, comm=comm)
+    for _ in range(args.warmup):
+        res = step()
+    torch.cuda.synchronize()
+    if args.exchange != "splitters":
+        comm.sent_bytes, comm.p2p_rounds, comm.exchange_s = 0, 0, 0.0
+        comm.timed = True
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+    torch.cuda.synchronize()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    elapsed = float(tt.item())
+    if args.exchange == "splitters":  # the last step's range, viewed in the comm's buffer
+        res = ls.DistComm.view(*res, owner=dcomm)
+        dphase, dsent = dcomm.timing()
+        dcoll = dcomm.collectives()
+    # global check: every range sorted, boundaries ordered, multiset preserved
+    nres = res.numel()
+    cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+    ls.count_descents(res, nres, cnt, key=key)
+    edges = ((torch.stack([res[0], res[-1]]).to(torch.int64) & 0xFFFFFFFF)).to(cdev) if nres else \
+        torch.tensor([2**33, -1], dtype=torch.int64, device=cdev)  # empty range: neutral for the order check
+    allg = [torch.empty_like(edges) for _ in range(world)]
+    dist.all_gather(allg, edges)
+    h_in = torch.zeros(1024, dtype=torch.int32, device=dev)
+    h_out = torch.zeros(1024, dtype=torch.int32, device=dev)
+    ls.histogram(src, m, h_in, key=key)
+    ls.histogram(res, nres, h_out, key=key)
+    s_in = (src[:m].to(torch.int64) & 0xFFFFFFFF).sum()
+    s_out = (res.to(torch.int64) & 0xFFFFFFFF).sum()
+    red = torch.stack([s_in, s_out]).to(cdev)
+    h_in, h_out = h_in.to(cdev), h_out.to(cdev)
+    dist.all_reduce(h_in)
+    dist.all_reduce(h_out)
+    dist.all_reduce(red)
+    ok = int(cnt.item()) == 0 and torch.equal(h_in, h_out) and int(red[0]) == int(red[1])
+    lastmax = -1
+    for e in allg:  # ranges in rank order: each range's first key >= every earlier key
+        if int(e[0]) > 2**32:
+            continue
+        ok = ok and int(e[0]) >= lastmax
+        lastmax = int(e[1])
+    okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    ok = bool(okt.item())
+    # exchange statistics: max over ranks (last step); the plan's work and wait
+    ph_names = ("local_sort", "plan", "plan_work", "plan_wait", "exchange", "merge")
+    if args.exchange == "splitters":
+        vals = [float(dsent), dphase["exchange"] * 1e6, 1.0] + [dphase[k] * 1e6 for k in ph_names]
+    else:
+        vals = [comm.sent_bytes / args.steps, comm.exchange_s * 1e9 / args.steps, comm.p2p_rounds / args.steps] + \
+            [0.0] * len(ph_names)
+    st = torch.tensor(vals, dtype=torch.float64, device=cdev)
+    dist.all_reduce(st, op=dist.ReduceOp.MAX)
+    sent, exs, rounds = float(st[0]), float(st[1]) / 1e9, float(st[2])
+    links = world - 1 if args.exchange == "splitters" else 1
+    xgmi = {"bytes_sent_per_rank_per_step": int(sent), "p2p_rounds_per_step": rounds,
+            "exchange_ms_per_step": round(exs * 1e3, 4), "links_per_round": links,
+            "per_link_GBps": round(sent / links / exs / 1e9, 2) if exs > 0 else None,
+            "note": ("max over ranks, last step; exchange = device time of the grouped ncclSend/ncclRecv "
+                     "(labsort_dist_timing); plan_wait = time inside the plan's collectives (waiting for "
+                     "the slowest rank), plan_work = the rest" if args.exchange == "splitters" else
+                     "max over ranks; exchange time is host wall time around the point-to-point calls")}
+    if args.exchange == "splitters":
+        xgmi["phases_ms_last_step"] = {k: round(float(st[3 + i]) / 1e6, 4) for i, k in enumerate(ph_names)}
+        # every rank's arrival at / return from each collective (ms since its call started)
+        mine = torch.tensor([v for k in ls.COLLECTIVES for v in dcoll[k]], dtype=torch.float64, device=cdev)
+        allc = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(allc, mine)
+        xgmi["collectives_ms_last_step"] = {
+            k: [[round(float(allc[r][2 * i]), 3), round(float(allc[r][2 * i + 1]), 3)] for r in range(world)]
+            for i, k in enumerate(ls.COLLECTIVES) if any(float(allc[r][2 * i]) >= 0 for r in range(world))}
+    del src, res
+    return {"elapsed": elapsed, "ok": ok, "xgmi": xgmi, "keys": sum(sizes)}
+
+
+def dist_main(args, torch, ls, world, rank, dev):
+    """N > 1 (one process per GPU under torch.distributed.run): BASELINE config 5 -- a
+    2^total-log2n-key array (default 2^30) partitioned over the N ranks (2^30 / N keys
+    each: strong scaling) and sorted by the product's distributed merge sort; then, as a
+    secondary field, the same schedule with 2^log2n keys per rank (weak scaling)."""
+    import torch.distributed as dist
+    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # where collectives' tensors live
+    if args.backend == "nccl":
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dist.init_process_group("gloo")
+    dmod = importlib.import_module(PKG_NAME + ".dist")
+    stream = torch.cuda.Stream(device=dev)
+    dcomm = dmod.make_comm(ls, backend=args.backend) if args.exchange == "splitters" else None
+    comm = None
+    if args.exchange != "splitters":
+        comm = dmod.P2PComm() if args.backend == "nccl" else dmod.HostStagedComm()
+    total = 1 << args.total_log2n
+    strong = dist_leg(torch, ls, dmod, args, dev, cdev, stream, rank, world,
+                      [total * (r + 1) // world - total * r // world for r in range(world)], SEED + 5, dcomm, comm)
+    weak = None
+    if not args.no_weak:
+        weak = dist_leg(torch, ls, dmod, args, dev, cdev, stream, rank, world, [1 << args.log2n] * world,
+                        SEED + 5, dcomm, comm)
+    if not (strong["ok"] and (weak is None or weak["ok"])):
+        print(f"bench.py: rank {rank}: OUTPUT CHECK FAILED (sort result is not a sorted permutation)", file=sys.stderr)
+        sys.exit(3)
+    dist.barrier()
+    if dcomm is not None:
+        dcomm.close()
+    dist.destroy_process_group()
+    # the host-pointer leg runs once every rank is done with its GPU
+    hostp = host_leg(args) if rank == 0 and not args.no_host_path and args.backend == "nccl" else None
+    if rank != 0:
+        return
+    how = ("splitter exchange (labsort_dist_sort: pairwise ncclSend/ncclRecv to all peers at once, merge of "
+           "the received runs)" if args.exchange == "splitters" else "bitonic pairwise merge-split network")
+    line = {
+        "metric": "Mkeys/s sorting uint32, n=2^28, 1 GPU (+ merge-sort at 2/4/8)",
+        "value": round(strong["keys"] * args.steps / strong["elapsed"] / 1e6, 2), "unit": "Mkeys/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(strong["elapsed"] / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (counter-based splitmix64 generator on device)",
+        "config": {"workload": f"BASELINE config 5: n=2^{args.total_log2n} uint32 merge sort partitioned across "
+                               f"{world} GPUs (2^{args.total_log2n}/{world} keys per rank): local radix sort + {how} "
+                               f"over {'RCCL/xGMI' if args.backend == 'nccl' else 'gloo host collectives (rehearsal)'}",
+                   "n_total": strong["keys"], "n_per_gpu": strong["keys"] // world, "algo": "merge",
+                   "local_algo": "radix", "key": "u32", "dist": args.dist,
+                   "parallelism": f"{world} ranks, {'RCCL' if args.backend == 'nccl' else 'gloo'} {args.exchange} exchange"},
+        "verified": "sorted permutation (descents, digit histograms, sums), ranges in rank order",
+        "xgmi": strong["xgmi"], "roofline": None, "cpu_baseline": None,
+    }
+    if weak:
+        line["weak"] = {"workload": f"the same schedule with 2^{args.log2n} keys per GPU (weak scaling)",
+                        "value": round(weak["keys"] * args.steps / weak["elapsed"] / 1e6, 2), "unit": "Mkeys/s",
+                        "ms_per_step": round(weak["elapsed"] / args.steps * 1e3, 4), "scaling": "weak",
+                        "xgmi": weak["xgmi"]}
+    if hostp:
+        line["host_path"] = hostp
+    print(json.dumps(line), flush=True)
+
+
 def main():
     args = parse()
     if args.host_leg:
@@ -390,45 +563,18 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)  # ranks share a device only in the gloo test mode
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    cdev = dev if args.backend == "nccl" else torch.device("cpu")  # where collectives' tensors live
     if REPO not in sys.path:
         sys.path.insert(0, REPO)
     ls = importlib.import_module(PKG_NAME)
+    if world > 1:
+        return dist_main(args, torch, ls, world, rank, dev)
 
     n = 1 << args.log2n
     key = "u32"
     stream = torch.cuda.Stream(device=dev)
     ws = None
 
-    if world > 1:
-        import torch.distributed as dist
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
-        dmod = importlib.import_module(PKG_NAME + ".dist")
-        src = torch.empty(n, dtype=torch.int32, device=dev)
-        with torch.cuda.stream(stream):
-            ls.fill(src, n, SEED + 5, args.dist, first=rank * n, stream=stream)
-        if args.exchange == "splitters":
-            # the product: labsort_dist_sort (csrc/dist_plan.h's schedule in C++) on this
-            # rank's communicator -- RCCL (ncclCommInitRank) or, backend gloo, host-staged
-            dcomm = dmod.make_comm(ls, backend=args.backend)
-
-            def step():
-                ptr, cnt, _ = dcomm.sort(src, n, key=key, stream=stream)
-                return ptr, cnt
-        else:
-            comm = dmod.P2PComm() if args.backend == "nccl" else dmod.HostStagedComm()
-            ops = dmod.HipOps(ls, key=key, local_algo="radix", stream=stream)
-
-            def step():
-                with torch.cuda.stream(stream):
-                    return dmod.dist_sort(src, ops, copy_input=True, comm=comm)
-
-        def barrier():
-            dist.barrier()
-    elif args.algo == "pairs":
+    if args.algo == "pairs":
         src = torch.empty(n, dtype=torch.int32, device=dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
         vsrc = torch.arange(n, dtype=torch.int32, device=dev)
@@ -439,9 +585,6 @@ def main():
         def step():
             ls.sort_pairs_device(src, vsrc, out, vout, n, key=key, algo=args.pair_algo, workspace=ws, stream=stream)
             return out
-
-        def barrier():
-            pass
     else:
         src = torch.empty(n, dtype=torch.int32, device=dev)
         out = torch.empty(n, dtype=torch.int32, device=dev)
@@ -452,13 +595,8 @@ def main():
             ls.sort_device(src, out, n, key=key, algo=args.algo, workspace=ws, stream=stream)
             return out
 
-        def barrier():
-            pass
-
     def status():
         """the kernels' own error report for the last sort (raises LabsortError)"""
-        if world > 1:
-            return  # HipOps.local_sort checks it after every local sort
         if args.algo == "pairs":
             ls.pairs_workspace_status(ws, n, args.pair_algo, stream=stream)
         else:
@@ -472,75 +610,29 @@ def main():
 
     dom = "onesweep" if args.algo in ("radix", "radix1") or (args.algo == "pairs" and args.pair_algo == "radix") \
         else "merge"
-    if args.algo == "radix" and world == 1 and ls.radix_impl(n) == "gather":
+    if args.algo == "radix" and ls.radix_impl(n) == "gather":
         dom = "gsweep"  # the gathered passes (2^16 <= n < 2^25)
-    if args.algo == "radix" and world == 1 and ls.radix_impl(n) == "small":
-        dom = "small"  # the single-launch sort (n <= 2^22)
-    if world > 1 and args.exchange != "splitters":
-        comm.sent_bytes, comm.p2p_rounds, comm.exchange_s = 0, 0, 0.0
-        comm.timed = True
     ls.timing_enable(True)
-    barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = step()
     torch.cuda.synchronize()
-    barrier()
     t1 = time.perf_counter()
     k_ms, k_cnt = ls.timing_read(dom)
     ls.timing_enable(False)
     elapsed = t1 - t0
     status()
 
-    if world > 1:
-        import torch.distributed as dist
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
-        if args.exchange == "splitters":  # the last step's range, viewed in the comm's buffer
-            res = ls.DistComm.view(*res)
-            dphase, dsent = dcomm.timing()
-        # global check: every shard sorted, boundaries ordered, multiset preserved
-        nres = res.numel()  # the splitter exchange leaves ranges of slightly different sizes
-        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
-        ls.count_descents(res, nres, cnt, key=key)
-        f = 0x80000000 if key == "i32" else 0
-        edges = ((torch.stack([res[0], res[-1]]).to(torch.int64) & 0xFFFFFFFF) ^ f).to(cdev) if nres else \
-            torch.tensor([2**33, -1], dtype=torch.int64, device=cdev)  # empty range: neutral for the order check
-        allg = [torch.empty_like(edges) for _ in range(world)]
-        dist.all_gather(allg, edges)
-        h_in = torch.zeros(1024, dtype=torch.int32, device=dev)
-        h_out = torch.zeros(1024, dtype=torch.int32, device=dev)
-        ls.histogram(src, n, h_in, key=key)
-        ls.histogram(res, nres, h_out, key=key)
-        s_in = (src.to(torch.int64) & 0xFFFFFFFF).sum()
-        s_out = (res.to(torch.int64) & 0xFFFFFFFF).sum()
-        red = torch.stack([s_in, s_out]).to(cdev)
-        h_in, h_out = h_in.to(cdev), h_out.to(cdev)
-        dist.all_reduce(h_in)
-        dist.all_reduce(h_out)
-        dist.all_reduce(red)
-        ok = int(cnt.item()) == 0 and torch.equal(h_in, h_out) and int(red[0]) == int(red[1])
-        lastmax = -1
-        for e in allg:  # ranges in rank order: each range's first key >= every earlier key
-            if int(e[0]) > 2**32:
-                continue
-            ok = ok and int(e[0]) >= lastmax
-            lastmax = int(e[1])
-        okt = torch.tensor([1 if ok else 0], dtype=torch.int32, device=cdev)
-        dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-        ok = bool(okt.item())
-    else:
-        ok, desc = verify(torch, ls, src, res, n, key)
-        if ok and args.algo == "pairs":
-            # each payload is its key's input index: the gather reproduces the output keys,
-            # and equal keys keep ascending indices (stable)
-            idx = vout.to(torch.int64)
-            ok = bool((idx >= 0).all()) and bool((idx < n).all()) and torch.equal(src[idx], res)
-            if ok and n > 1:
-                ok = bool(((vout[1:] > vout[:-1]) | (res[1:] != res[:-1])).all())
-            del idx
+    ok, desc = verify(torch, ls, src, res, n, key)
+    if ok and args.algo == "pairs":
+        # each payload is its key's input index: the gather reproduces the output keys,
+        # and equal keys keep ascending indices (stable)
+        idx = vout.to(torch.int64)
+        ok = bool((idx >= 0).all()) and bool((idx < n).all()) and torch.equal(src[idx], res)
+        if ok and n > 1:
+            ok = bool(((vout[1:] > vout[:-1]) | (res[1:] != res[:-1])).all())
+        del idx
     if not ok:
         print(f"bench.py: rank {rank}: OUTPUT CHECK FAILED (sort result is not a sorted permutation)",
               file=sys.stderr)
@@ -549,7 +641,7 @@ def main():
     # config 4 beside the headline: the merge sort of the same device input (N = 1,
     # radix headline only); its own verification, status check and kernel timings
     merge_leg = None
-    if world == 1 and args.algo == "radix" and not args.no_merge:
+    if args.algo == "radix" and not args.no_merge:
         mws = torch.empty(max(ls.workspace_bytes(n, "merge"), 256), dtype=torch.uint8, device=dev)
         mout = torch.empty_like(src)
 
@@ -598,7 +690,7 @@ def main():
     # BASELINE config 2 beside the headline: 2^20 keys, radix (the gathered passes at this
     # size), device-resident, verified; launch-bound, so reported as time per sort
     config2 = None
-    if world == 1 and args.algo == "radix" and not args.no_merge and n > (1 << 20):
+    if args.algo == "radix" and not args.no_merge and n > (1 << 20):
         n2 = 1 << 20
         s2 = torch.empty(n2, dtype=torch.int32, device=dev)
         o2 = torch.empty_like(s2)
@@ -627,7 +719,7 @@ def main():
     # SURVEY 8f row 4 beside the headline: the stable key/value radix sort of the same keys
     # with 4-byte payloads (each its input index), verified as the pairs run is
     pairs_leg = None
-    if world == 1 and args.algo == "radix" and not args.no_merge:
+    if args.algo == "radix" and not args.no_merge:
         vin = torch.arange(n, dtype=torch.int32, device=dev)
         pko = torch.empty_like(src)
         pvo = torch.empty_like(src)
@@ -671,130 +763,88 @@ def main():
         del vin, pko, pvo, pws
 
     config1 = None
-    if world == 1 and args.algo == "radix" and not args.no_merge:
+    if args.algo == "radix" and not args.no_merge:
         config1 = config1_gpu(ls, torch, dev, stream)
         if config1["verified"] != "fixture":
             print("bench.py: CONFIG 1 OUTPUT CHECK FAILED", file=sys.stderr)
             sys.exit(3)
 
-    total_keys = n * world * args.steps
-    value = total_keys / elapsed / 1e6
+    value = n * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
-    xgmi = None
-    if world > 1:
-        import torch.distributed as dist
-        if args.exchange == "splitters":
-            vals = [float(dsent), dphase["exchange"] * 1e6, 1.0] + [dphase[k] * 1e6 for k in
-                                                                    ("local_sort", "plan", "exchange", "merge")]
-        else:
-            vals = [comm.sent_bytes / args.steps, comm.exchange_s * 1e9 / args.steps, comm.p2p_rounds / args.steps,
-                    0.0, 0.0, 0.0, 0.0]
-        st = torch.tensor(vals, dtype=torch.float64, device=cdev)
-        dist.all_reduce(st, op=dist.ReduceOp.MAX)
-        sent, exs, rounds = float(st[0]), float(st[1]) / 1e9, float(st[2])
-        links = world - 1 if args.exchange == "splitters" else 1
-        xgmi = {"bytes_sent_per_rank_per_step": int(sent), "p2p_rounds_per_step": rounds,
-                "exchange_ms_per_step": round(exs * 1e3, 4),
-                "links_per_round": links,
-                "per_link_GBps": round(sent / links / exs / 1e9, 2) if exs > 0 else None,
-                "note": ("max over ranks, last step; exchange = device time of the grouped ncclSend/ncclRecv "
-                         "(labsort_dist_timing)" if args.exchange == "splitters" else
-                         "max over ranks; exchange time is host wall time around the point-to-point calls "
-                         "(stream synchronised on both sides)")}
-        if args.exchange == "splitters":
-            xgmi["phases_ms_last_step"] = {k: round(float(st[3 + i]) / 1e6, 4) for i, k in
-                                           enumerate(("local_sort", "plan", "exchange", "merge"))}
+    # the host-pointer leg (PCIe-inclusive, child processes)
+    hostp = host_leg(args) if not args.no_host_path else None
 
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
-        if args.exchange == "splitters":
-            del res
-            dcomm.close()
-        dist.destroy_process_group()
-    # the host-pointer leg runs once every rank is done with its GPU
-    hostp = host_leg(args) if rank == 0 and not args.no_host_path and args.backend == "nccl" else None
+    # the copy ceiling: the library's streaming copy (labsort_copy: 16-B nontemporal loads
+    # and stores in 16384-word tiles, one workgroup per CU) of the same n keys, each of 5
+    # launches timed by HIP events on the stream it runs on; the median launch
+    cp = torch.empty_like(src)
+    for _ in range(2):
+        ls.copy(src, cp, n, stream=stream)
+    times = []
+    for _ in range(5):
+        ls.timing_enable(True)
+        ls.copy(src, cp, n, stream=stream)
+        torch.cuda.synchronize()
+        times.append(ls.timing_read("copy")[0])
+        ls.timing_enable(False)
+    copy_ms = sorted(times)[len(times) // 2]
+    copy_gbs = 8.0 * n / (copy_ms * 1e-3) / 1e9
+    copy_ok = torch.equal(cp, src)
+    del cp
 
-    # the measured copy ceiling: a device-to-device copy of the same n keys (torch copy_,
-    # i.e. hipMemcpy D2D), the practical HBM rate a read-once write-once pass can reach
-    copy_gbs = None
-    if rank == 0 and world == 1:
-        cp = torch.empty_like(src)
-        for _ in range(3):
-            cp.copy_(src)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(10):
-            cp.copy_(src)
-        e1.record()
-        e1.synchronize()
-        copy_gbs = 8.0 * n * 10 / (e0.elapsed_time(e1) * 1e-3) / 1e9
-        del cp
-
-    if rank == 0:
-        avg_ms = k_ms / k_cnt if k_cnt else None
-        per_launch_bytes = 16.0 * n if args.algo == "pairs" else 8.0 * n  # key (+ payload) read + written
-        achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms else None
-        traffic, tsrc = pmc_traffic(dom, n)
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                    "traffic": traffic, "kernel": ("k_onesweep_p" if dom == "onesweep" and args.algo == "radix" else
-                               "k_gsweep" if dom == "gsweep" else
-                               "k_onesweep<8, KV>" if args.algo == "pairs" and dom == "onesweep" else f"k_{dom}"), "launches": k_cnt,
-                    "avg_launch_ms": round(avg_ms, 5) if avg_ms else None,
-                    "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
-        if copy_gbs and achieved:
-            roofline["copy_ceiling"] = {"value": round(copy_gbs, 1), "unit": "GB/s", "frac": round(achieved / copy_gbs, 4),
-                                        "probe": "device-to-device copy of the same n keys (torch copy_ = hipMemcpy "
-                                                 "D2D, 10 runs, read + write bytes), same box, after the timed region"}
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_seconds, n, ls)
-            cpu["config1"] = config1_cpu(ls)
-        wl = {"radix": "LSD radix sort (8-bit digits, onesweep)", "merge": "LDS tile sort + merge-path passes",
-              "radix1": "LSD radix with 1-bit split passes (letra.pdf)",
-              "pairs": "stable key/value sort (uint32 key + uint32 index payload): " + (
-                  "8-bit LSD onesweep passes" if args.pair_algo == "radix" else "LDS tile sort + merge-path passes")
-              }[args.algo]
-        if world > 1:
-            how = ("splitter exchange (labsort_dist_sort: pairwise ncclSend/ncclRecv to all peers at once, merge of "
-                   "the received runs)" if args.exchange == "splitters" else "bitonic pairwise merge-split network")
-            workload = (f"merge sort across {world} GPUs: local radix sort of 2^{args.log2n} uint32 keys per GPU "
-                        f"+ {how} over RCCL/xGMI (BASELINE config 5 shape, weak scaling)")
-        else:
-            workload = f"{wl}, n=2^{args.log2n} uint32 {args.dist}, device-resident (BASELINE config 3)"
-        line = {
-            "metric": "Mkeys/s sorting uint32, n=2^28, 1 GPU (+ merge-sort at 2/4/8)",
-            "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "u32",
-            "data": "synthetic (counter-based splitmix64 generator on device)",
-            "config": {"workload": workload, "n_per_gpu": n, "algo": args.algo if world == 1 else "merge",
-                       "key": key, "dist": args.dist,
-                       "parallelism": "single GPU" if world == 1 else f"{world} ranks, RCCL {args.exchange} exchange"},
-            "verified": "sorted permutation (descents, digit histograms, sums)" + (
-                "; payloads gather the output keys, stable" if args.algo == "pairs" and world == 1 else ""),
-            "roofline": roofline, "cpu_baseline": cpu,
-        }
-        if copy_gbs:  # each leg's dominant kernel against the same measured copy rate
-            for leg in (merge_leg and merge_leg["roofline"], merge_leg and merge_leg["tile_sort"],
-                        pairs_leg and pairs_leg["roofline"]):
-                if leg and leg.get("achieved"):
-                    leg["copy_frac"] = round(leg["achieved"] / copy_gbs, 4)
-        if merge_leg:
-            line["merge"] = merge_leg
-        if config1:
-            line["config1"] = config1
-        if config2:
-            line["config2"] = config2
-        if pairs_leg:
-            line["pairs"] = pairs_leg
-        if xgmi:
-            line["config"]["local_algo"] = "radix"
-            line["xgmi"] = xgmi
-        if hostp:
-            line["host_path"] = hostp
-        print(json.dumps(line), flush=True)
+    avg_ms = k_ms / k_cnt if k_cnt else None
+    per_launch_bytes = 16.0 * n if args.algo == "pairs" else 8.0 * n  # key (+ payload) read + written
+    achieved = per_launch_bytes / (avg_ms * 1e-3) / 1e9 if avg_ms else None
+    traffic, tsrc = pmc_traffic(dom, n)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1) if achieved else None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                "traffic": traffic, "kernel": ("k_onesweep_p" if dom == "onesweep" and args.algo == "radix" else
+                                               "k_gsweep" if dom == "gsweep" else
+                                               "k_onesweep_p<true>" if args.algo == "pairs" and dom == "onesweep"
+                                               else f"k_{dom}"), "launches": k_cnt,
+                "avg_launch_ms": round(avg_ms, 5) if avg_ms else None,
+                "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
+    roofline["copy_ceiling"] = {
+        "value": round(copy_gbs, 1), "unit": "GB/s", "frac": round(achieved / copy_gbs, 4) if achieved else None,
+        "ms": round(copy_ms, 5), "verified": bool(copy_ok),
+        "probe": "labsort_copy of the same n keys (16-B nontemporal loads and stores, 16384-word tiles, one "
+                 "1024-thread workgroup per CU), median of 5 event-timed launches, after the timed region"}
+    cpu = None
+    if not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds, n, ls)
+        cpu["config1"] = config1_cpu(ls)
+    wl = {"radix": "LSD radix sort (8-bit digits, onesweep)", "merge": "LDS tile sort + merge-path passes",
+          "radix1": "LSD radix with 1-bit split passes (letra.pdf)",
+          "pairs": "stable key/value sort (uint32 key + uint32 index payload): " + (
+              "8-bit LSD onesweep passes" if args.pair_algo == "radix" else "LDS tile sort + merge-path passes")
+          }[args.algo]
+    line = {
+        "metric": "Mkeys/s sorting uint32, n=2^28, 1 GPU (+ merge-sort at 2/4/8)",
+        "value": round(value, 2), "unit": "Mkeys/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic (counter-based splitmix64 generator on device)",
+        "config": {"workload": f"{wl}, n=2^{args.log2n} uint32 {args.dist}, device-resident (BASELINE config 3)",
+                   "n_per_gpu": n, "algo": args.algo, "key": key, "dist": args.dist, "parallelism": "single GPU"},
+        "verified": "sorted permutation (descents, digit histograms, sums)" + (
+            "; payloads gather the output keys, stable" if args.algo == "pairs" else ""),
+        "roofline": roofline, "cpu_baseline": cpu,
+    }
+    for leg in (merge_leg and merge_leg["roofline"], merge_leg and merge_leg["tile_sort"],
+                pairs_leg and pairs_leg["roofline"]):  # each leg's dominant kernel against the same copy
+        if leg and leg.get("achieved"):
+            leg["copy_frac"] = round(leg["achieved"] / copy_gbs, 4)
+    if merge_leg:
+        line["merge"] = merge_leg
+    if config1:
+        line["config1"] = config1
+    if config2:
+        line["config2"] = config2
+    if pairs_leg:
+        line["pairs"] = pairs_leg
+    if hostp:
+        line["host_path"] = hostp
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

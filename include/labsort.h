@@ -39,12 +39,12 @@ extern "C" {
 #define LABSORT_ERR_ARG 1        /* bad argument (NULL, n too large, workspace too small) */
 #define LABSORT_ERR_HIP 2        /* a HIP runtime call failed: labsort_last_hip_error() */
 #define LABSORT_ERR_DEVICE 3     /* a kernel reported an internal error (bounded spin expired) */
+#define LABSORT_ERR_PEER 4       /* distributed sort: another rank failed (this one gave up with it) */
 
 /* algorithms */
 #define LABSORT_ALGO_RADIX 0     /* LSD radix, 8-bit digits: gathered passes for 2^16 <= n < 2^25,
                                     onesweep scatter passes outside (LABSORT_RADIX_IMPL=onesweep or
-                                    =gather forces one; =small: one cooperative launch for
-                                    labsort_tile_keys() < n <= 2^22, small.hip) */
+                                    =gather forces one) */
 #define LABSORT_ALGO_MERGE 1     /* LDS tile radix + merge-path merge passes */
 #define LABSORT_ALGO_RADIX1 2    /* LSD radix with 1-bit digits: letra.pdf's split, 32 passes */
 #define LABSORT_ALGO_AUTO 3      /* MERGE for n <= LABSORT_AUTO_MERGE_MAX_KEYS (fewer launches and
@@ -53,6 +53,10 @@ extern "C" {
                                     default of the host drop-ins order_array / sort (LABSORT_ALGO
                                     env overrides) */
 #define LABSORT_AUTO_MERGE_MAX_KEYS (1u << 16) /* r27: the fused gathered radix wins from ~1.5 x 2^16 */
+/* key/value sorts (labsort_sort_pairs_device, AUTO): merge up to here.  Their radix has no
+   fused small path (histogram, plan and four persistent passes at every size), so they keep
+   the r19 crossover measured before the keys-only threshold moved */
+#define LABSORT_AUTO_PAIRS_MERGE_MAX_KEYS (1u << 18)
 
 /* key types: how the 32-bit words are ordered */
 #define LABSORT_KEY_U32 0
@@ -76,8 +80,9 @@ extern "C" {
 #define LABSORT_K_PARTITION 4
 #define LABSORT_K_GSWEEP 5       /* gathered radix pass (LABSORT_ALGO_RADIX, 2^16 <= n < 2^25) */
 #define LABSORT_K_GCOPY 6        /* its final gathered copy */
-#define LABSORT_K_SMALL 7        /* single-launch radix sort (LABSORT_ALGO_RADIX, n <= 2^22) */
-#define LABSORT_K_COUNT 8
+#define LABSORT_K_LSWEEP 7       /* the local first pass of the onesweep radix (k_lsweep) */
+#define LABSORT_K_COPY 8         /* the streaming copy (labsort_copy: the bench's copy ceiling) */
+#define LABSORT_K_COUNT 9
 
 /* ---- library info ---- */
 const char *labsort_version(void);
@@ -138,12 +143,21 @@ int labsort_pairs_workspace_status(const void *d_workspace, size_t n, int algo, 
 #define LABSORT_MULTI_MAX_RANKS 8
 /* phases of labsort_multi_timing / labsort_dist_timing, ms of the last call (device
  * timeline, max over ranks; phases may overlap): 0 H2D (host input), 1 local sort,
- * 2 samples + splitters + cut points, 3 exchange, 4 merge, 5 D2H tail after the
- * merge (host output), 6 total (host wall time) */
-#define LABSORT_MULTI_PHASES 7
+ * 2 plan (samples + splitters + cut points, collectives included), 3 exchange, 4 merge,
+ * 5 D2H tail after the merge (host output), 6 total (host wall time), 7 the plan's own
+ * work (phase 2 minus the time spent inside its collectives), 8 the plan's wait (time
+ * inside the collectives: mostly waiting for the slowest rank to arrive) */
+#define LABSORT_MULTI_PHASES 9
+/* Collectives of one schedule call, in order: 0 samples (allgather), 1 piece counts
+ * (allgather), 2 buffer growth (allgather; runs only when a range outgrew the pre-sized
+ * receive buffer).  labsort_multi_collectives / labsort_dist_collectives: host wall clock
+ * (ms since the rank's call started) at which each rank arrived at / returned from each
+ * of them in the last call (-1: did not run); arrive[r * ncoll + k], leave[r * ncoll + k]. */
+#define LABSORT_MULTI_COLLECTIVES 3
 int labsort_sort_host_multi(void *h_keys, size_t n, int key_type, int ngpus);  /* devices 0..ngpus-1 */
 int labsort_sort_host_ranks(void *h_keys, size_t n, int key_type, int nranks, const int *devices, int transport);
 int labsort_multi_timing(double *phase_ms, int nphases, size_t *max_sent_bytes);
+int labsort_multi_collectives(double *arrive, double *leave, int nranks, int ncoll);
 int labsort_multi_last_hip_error(void);
 /* keys of each rank's range of the sorted array in the last call (ranks in order) */
 int labsort_multi_range_counts(size_t *counts, int nranks);
@@ -161,8 +175,13 @@ int labsort_multi_plan(const uint32_t *const *h_shards, const size_t *m, int nra
  *         broadcast by the caller's own means, every rank calls labsort_comm_init_rccl
  *         with its device current (ncclCommInitRank).
  *   Host callbacks: the collectives are the caller's (labsort_host_coll over host
- *         buffers; device pieces are staged): several ranks may share a GPU (tests). */
+ *         buffers; device pieces are staged): several ranks may share a GPU (tests).
+ * A rank whose own step fails (local sort, samples, bounds, buffers) still reports its
+ * status in every collective up to the exchange, so every rank returns an error together
+ * (the failed one its own, the others LABSORT_ERR_PEER) instead of waiting for it. */
 #define LABSORT_COMM_ID_BYTES 128
+/* ranks of one communicator: the receive-side merge takes two halves of at most 8 runs */
+#define LABSORT_DIST_MAX_RANKS 16
 typedef struct labsort_comm *labsort_comm_t;
 typedef struct {
     void *ctx;
@@ -185,6 +204,8 @@ int labsort_comm_destroy(labsort_comm_t comm);
 int labsort_dist_sort(labsort_comm_t comm, const void *d_keys, size_t m, int key_type, void *stream,
                       const void **d_result, size_t *count, size_t *global_offset);
 int labsort_dist_timing(labsort_comm_t comm, double *phase_ms, int nphases, size_t *sent_bytes);
+/* this rank's arrival / return times at the collectives of its last sort (ncoll entries) */
+int labsort_dist_collectives(labsort_comm_t comm, double *arrive, double *leave, int ncoll);
 int labsort_dist_last_hip_error(labsort_comm_t comm);
 
 /* ---- key/value (sort_by_key; no lab.cu counterpart, the reference sorts
@@ -195,7 +216,7 @@ int labsort_dist_last_hip_error(labsort_comm_t comm);
  * stable argsort, from which payloads of any width can be gathered.
  * algo: LABSORT_ALGO_RADIX (8-bit LSD onesweep passes carrying the payload),
  * LABSORT_ALGO_MERGE (LDS tile sort of labsort_pair_tile_keys() pairs + merge-path
- * passes) or LABSORT_ALGO_AUTO (merge up to LABSORT_AUTO_MERGE_MAX_KEYS, radix above).
+ * passes) or LABSORT_ALGO_AUTO (merge up to LABSORT_AUTO_PAIRS_MERGE_MAX_KEYS, radix above).
  * Asynchronous on `stream`, no allocation; d_ws >= labsort_pairs_workspace_bytes(n, algo). */
 size_t labsort_pair_tile_keys(void);
 size_t labsort_pairs_workspace_bytes(size_t n, int algo);
@@ -221,14 +242,12 @@ int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *
 /* Merge of up to 8 sorted runs lying back to back in d_in: run q =
  * d_in[h_offsets[q] .. h_offsets[q+1]), q < nruns (host array of nruns+1 offsets).
  * Writes the merged keys to d_out[h_offsets[0] .. h_offsets[nruns]) (d_out != d_in);
- * equal keys keep run order (stable).  Default: ceil(log2 nruns) levels of pairwise
- * merge-path passes over explicit pairs of runs (k_merge_pass_p, one launch per pair),
- * ping-ponging through the workspace so the last level writes d_out;
- * LABSORT_MERGE_RUNS=kway: one K-way pass instead (kmerge.hip, slower on MI355X:
- * DESIGN.md §3.2).  Generalises separators_kernel + merge_segments_kernel
- * (lab.cu:209-300) from 2 to K runs; the multi-GPU schedule merges the runs a rank
- * receives with it.  d_ws: >= labsort_merge_runs_workspace_bytes(h_offsets[nruns])
- * (the larger of the ping-pong keys and the K-way pass's cuts). */
+ * equal keys keep run order (stable): ceil(log2 nruns) levels of pairwise merge-path
+ * passes over explicit pairs of runs (k_merge_pass_p, one launch per pair),
+ * ping-ponging through the workspace so the last level writes d_out.  Generalises
+ * separators_kernel + merge_segments_kernel (lab.cu:209-300) from 2 to K runs; the
+ * multi-GPU schedule merges the runs a rank receives with it.
+ * d_ws: >= labsort_merge_runs_workspace_bytes(h_offsets[nruns]) (ping-pong keys). */
 size_t labsort_merge_runs_workspace_bytes(size_t n);
 int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, int nruns, int key_type,
                        void *d_workspace, size_t ws_bytes, void *stream);
@@ -245,6 +264,10 @@ int labsort_upper_bound(const void *d_sorted, size_t n, int key_type, const uint
 /* ---- utilities ---- */
 /* Counter-based generator, identical to oracle_fill: keys first..first+n-1. */
 int labsort_fill(void *d_out, size_t n, uint64_t seed, int dist, uint64_t param, uint64_t first, void *stream);
+/* d_out[0..n) = d_in[0..n) (32-bit words): a streaming copy with 16-B nontemporal loads and
+ * stores in 16384-word tiles, one 1024-thread workgroup per CU -- the practical HBM rate of
+ * a read-once / write-once pass, which bench.py reports beside each kernel's roofline. */
+int labsort_copy(const void *d_in, void *d_out, size_t n, void *stream);
 /* *d_count += number of i with key[i] > key[i+1] (0 = sorted). */
 int labsort_count_descents(const void *d_keys, size_t n, int key_type, uint32_t *d_count, void *stream);
 

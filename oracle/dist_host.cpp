@@ -43,7 +43,7 @@ struct HostOps {
         return LABSORT_OK;
     }
     int recv_buffer(uint64_t total, uint32_t **recv) {
-        R.assign(total ? total : 1, 0u);
+        if (R.size() < total || R.empty()) R.resize(total ? total : 1, 0u);
         *recv = R.data();
         return LABSORT_OK;
     }

@@ -26,12 +26,12 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 # LABSORT_LIBRARY: path of an alternative build (diagnostic builds under harness/exp)
 LIB_PATH = os.environ.get("LABSORT_LIBRARY") or os.path.join(HERE, "liblabsort.so")
 
-OK, ERR_ARG, ERR_HIP, ERR_DEVICE = 0, 1, 2, 3
+OK, ERR_ARG, ERR_HIP, ERR_DEVICE, ERR_PEER = 0, 1, 2, 3, 4
 ALGO = {"radix": 0, "merge": 1, "radix1": 2, "auto": 3}
 KEY = {"u32": 0, "i32": 1}
 DIST = {"u32": 0, "u31": 1, "mod100": 2, "mod1000": 3, "sorted": 4, "reversed": 5, "const": 6, "lowbits": 7}
 KCLASS = {"histogram": 0, "onesweep": 1, "tile_sort": 2, "merge": 3, "partition": 4, "gsweep": 5, "gcopy": 6,
-          "small": 7}
+          "lsweep": 7, "copy": 8}
 
 # exported symbols of include/labsort.h + lab.h (checked by tests/test_abi.py)
 C_SYMBOLS = [
@@ -47,14 +47,21 @@ C_SYMBOLS = [
     "labsort_multi_plan", "labsort_multi_error_detail", "labsort_multi_range_counts",
     "labsort_comm_unique_id", "labsort_comm_init_rccl", "labsort_comm_init_host", "labsort_comm_destroy",
     "labsort_dist_sort", "labsort_dist_timing", "labsort_dist_last_hip_error",
+    "labsort_multi_collectives", "labsort_dist_collectives", "labsort_copy",
 ]
 XFER = {"auto": 0, "rccl": 1, "peer": 2}
-MULTI_PHASES = ["h2d", "local_sort", "plan", "exchange", "merge", "d2h", "total"]
+MULTI_PHASES = ["h2d", "local_sort", "plan", "exchange", "merge", "d2h", "total", "plan_work", "plan_wait"]
+COLLECTIVES = ["samples", "counts", "grow"]  # the schedule's collectives, in order (labsort.h)
 CXX_SYMBOLS = ["_Z11order_arrayPii", "_Z16order_with_trustPii"]
 
 
 class LabsortError(RuntimeError):
-    pass
+    """A failed LABSORT_* status; .status holds the code (ERR_ARG, ERR_HIP, ERR_DEVICE,
+    ERR_PEER)."""
+
+    def __init__(self, msg: str, status: int = 0):
+        super().__init__(msg)
+        self.status = status
 
 
 # labsort_host_coll (include/labsort.h): host collectives supplied by the caller
@@ -152,6 +159,9 @@ def _load() -> ctypes.CDLL:
     L.labsort_dist_sort.argtypes = [p, p, sz, i, p, ctypes.POINTER(p), ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.labsort_dist_timing.argtypes = [p, ctypes.POINTER(ctypes.c_double), i, ctypes.POINTER(sz)]
     L.labsort_dist_last_hip_error.argtypes = [p]
+    L.labsort_multi_collectives.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), i, i]
+    L.labsort_dist_collectives.argtypes = [p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double), i]
+    L.labsort_copy.argtypes = [p, p, sz, p]
     L.labsort_pairs_workspace_status.argtypes = [p, sz, i, p]
     L.labsort_histogram.argtypes = [p, sz, i, i, p, p]
     L.labsort_fill.argtypes = [p, sz, u64, i, u64, u64, p]
@@ -182,7 +192,7 @@ def _check(status: int, what: str) -> None:
         msg = lib.labsort_error_string(status).decode()
         if status == ERR_HIP:
             msg += ": " + lib.labsort_hip_error_string(lib.labsort_last_hip_error()).decode()
-        raise LabsortError(f"{what} failed: {msg}")
+        raise LabsortError(f"{what} failed: {msg}", status)
 
 
 def _ptr(x) -> int:
@@ -236,7 +246,7 @@ def _check_multi(status: int, what: str) -> None:
     if status != OK:
         detail = lib.labsort_multi_error_detail().decode()
         raise LabsortError(f"{what} failed: {lib.labsort_error_string(status).decode()}"
-                           + (f" ({detail})" if detail else ""))
+                           + (f" ({detail})" if detail else ""), status)
 
 
 def sort_host_multi(a: np.ndarray, ngpus: int) -> None:
@@ -264,6 +274,15 @@ def multi_timing() -> tuple[dict, int]:
     sent = ctypes.c_size_t(0)
     _check(lib.labsort_multi_timing(ms, len(MULTI_PHASES), ctypes.byref(sent)), "multi_timing")
     return dict(zip(MULTI_PHASES, list(ms))), sent.value
+
+
+def multi_collectives(nranks: int) -> list:
+    """Per rank of the last multi-GPU host sort: {collective: (arrive_ms, leave_ms)} on the
+    host clock since that rank's start (-1: the collective did not run)."""
+    k = len(COLLECTIVES)
+    a, b = (ctypes.c_double * (nranks * k))(), (ctypes.c_double * (nranks * k))()
+    _check(lib.labsort_multi_collectives(a, b, nranks, k), "multi_collectives")
+    return [{COLLECTIVES[c]: (a[r * k + c], b[r * k + c]) for c in range(k)} for r in range(nranks)]
 
 
 def multi_range_counts(nranks: int) -> list:
@@ -326,16 +345,20 @@ class DistComm:
         _check_multi(st, "labsort_dist_sort")
         return res.value or 0, cnt.value, goff.value
 
-    def sort_tensor(self, d_keys, m: int, key: str = "u32", stream=None):
-        """As sort(), with the range as an int32 torch tensor viewing the communicator's
-        buffer (no copy; overwritten by the next sort) and its global offset."""
+    def sort_tensor(self, d_keys, m: int, key: str = "u32", stream=None, copy: bool = True):
+        """As sort(), with the range as an int32 torch tensor and its global offset.  By
+        default the range is copied out of the communicator's buffer; copy=False returns a
+        zero-copy view of that buffer instead, which keeps this communicator alive but is
+        overwritten by its next sort."""
         ptr, cnt, goff = self.sort(d_keys, m, key, stream)
-        return self.view(ptr, cnt), goff
+        v = self.view(ptr, cnt, owner=self)
+        return (v.clone() if copy else v), goff
 
     @staticmethod
-    def view(ptr: int, count: int):
+    def view(ptr: int, count: int, owner=None):
         """int32 torch tensor on the current device viewing `count` keys at device
-        address `ptr` (__cuda_array_interface__; no copy, no ownership)."""
+        address `ptr` (__cuda_array_interface__; no copy).  `owner` (e.g. the DistComm whose
+        buffer it is) is kept alive as long as the tensor."""
         import torch
         if count == 0:
             return torch.empty(0, dtype=torch.int32, device="cuda")
@@ -343,13 +366,24 @@ class DistComm:
         class _View:
             __cuda_array_interface__ = {"shape": (count,), "typestr": "<i4", "data": (ptr, False), "version": 2,
                                         "strides": None}
-        return torch.as_tensor(_View(), device="cuda")
+        holder = _View()
+        holder.owner = owner
+        t = torch.as_tensor(holder, device="cuda")
+        t._labsort_owner = holder  # the buffer's owner lives as long as the tensor
+        return t
 
     def timing(self) -> tuple[dict, int]:
         ms = (ctypes.c_double * len(MULTI_PHASES))()
         sent = ctypes.c_size_t(0)
         _check(lib.labsort_dist_timing(self.h, ms, len(MULTI_PHASES), ctypes.byref(sent)), "dist_timing")
         return dict(zip(MULTI_PHASES, list(ms))), sent.value
+
+    def collectives(self) -> dict:
+        """{collective: (arrive_ms, leave_ms)} of this rank's last sort (-1: not run)."""
+        k = len(COLLECTIVES)
+        a, b = (ctypes.c_double * k)(), (ctypes.c_double * k)()
+        _check(lib.labsort_dist_collectives(self.h, a, b, k), "dist_collectives")
+        return {COLLECTIVES[c]: (a[c], b[c]) for c in range(k)}
 
     def close(self) -> None:
         if self.h.value:
@@ -376,18 +410,14 @@ def workspace_bytes(n: int, algo: str = "radix") -> int:
 
 
 GS_MIN_N, GS_MAX_N = 1 << 16, 1 << 25  # LABSORT_ALGO_RADIX's gathered-pass window (common.h)
-SR_MAX_N = 1 << 22  # single-launch radix up to here (common.h SR_MAX_N)
 
 
 def radix_impl(n: int) -> str:
-    """Which LSD implementation LABSORT_ALGO_RADIX runs for n keys: "gather" (gsweep.hip),
-    "onesweep" (kernels.hip) or, with LABSORT_RADIX_IMPL=small and tile_keys() < n <= 2^22,
-    "small" (small.hip), as api.hip's use_small / use_gather decide."""
+    """Which LSD implementation LABSORT_ALGO_RADIX runs for n keys: "gather" (gsweep.hip)
+    or "onesweep" (lsweep.hip + kernels.hip), as api.hip's use_gather decides."""
     env = os.environ.get("LABSORT_RADIX_IMPL", "")
     if env == "gather":
         return "gather"
-    if tile_keys() < n <= SR_MAX_N and env == "small":
-        return "small"
     if GS_MIN_N <= n < GS_MAX_N and env != "onesweep":
         return "gather"
     return "onesweep"
@@ -514,6 +544,11 @@ def upper_bound(d_sorted, n: int, d_values, nv: int, d_out, key: str = "u32", st
     """d_out[i] = number of keys <= d_values[i] in the sorted run (key order)."""
     _check(lib.labsort_upper_bound(_ptr(d_sorted) if n else 0, n, KEY[key], _ptr(d_values), nv, _ptr(d_out),
                                    _stream(stream)), "upper_bound")
+
+
+def copy(d_in, d_out, n: int, stream=None) -> None:
+    """d_out[0..n) = d_in[0..n) (32-bit words) by the library's streaming copy kernel."""
+    _check(lib.labsort_copy(_ptr(d_in), _ptr(d_out), n, _stream(stream)), "copy")
 
 
 def count_descents(d_keys, n: int, d_count, key: str = "u32", stream=None) -> None:

@@ -130,7 +130,7 @@ RadixLayout radix_layout(size_t n, int bits, size_t tile) {
 }
 
 struct MergeLayout {
-    size_t off_tmp, off_part, off_km, total;
+    size_t off_tmp, off_part, total;
 };
 MergeLayout merge_layout(size_t n) {
     MergeLayout L{};
@@ -139,28 +139,18 @@ MergeLayout merge_layout(size_t n) {
     o = align_up(o + n * 4, 256);
     L.off_part = o;
     o = align_up(o + (labsort_merge_parts(n)) * 4, 256);
-    L.off_km = o;  // K-way merge samples and block cuts
-    o = align_up(o + km_workspace_words(n) * 4, 256);
     L.total = o;
     return L;
 }
 
-// LABSORT_ALGO_RADIX from GS_MIN_N keys on: the gathered passes (gsweep.hip), unless
-// LABSORT_RADIX_IMPL=onesweep selects the scatter passes (kernels.hip k_onesweep_p)
-bool use_small(size_t n);
+// LABSORT_ALGO_RADIX for GS_MIN_N <= n < GS_MAX_N: the gathered passes (gsweep.hip);
+// LABSORT_RADIX_IMPL=onesweep selects the scatter passes there too, =gather the
+// gathered passes at any n (tests)
 bool use_gather(size_t n) {
     const char *e = std::getenv("LABSORT_RADIX_IMPL");
-    if (e && !std::strcmp(e, "gather")) return true;  // any n (experiments, tests)
-    if (n < GS_MIN_N || n >= GS_MAX_N || use_small(n)) return false;
+    if (e && !std::strcmp(e, "gather")) return true;
+    if (n < GS_MIN_N || n >= GS_MAX_N) return false;
     return !(e && !std::strcmp(e, "onesweep"));
-}
-// LABSORT_RADIX_IMPL=small, TS_TILE < n <= SR_MAX_N: the single-launch sort (small.hip).
-// Not the default: at 2^20 it measured 0.094 ms (cooperative launch) against 0.082 for
-// the gathered passes
-bool use_small(size_t n) {
-    if (n <= (size_t)TS_TILE || n > SR_MAX_N) return false;
-    const char *e = std::getenv("LABSORT_RADIX_IMPL");
-    return e && !std::strcmp(e, "small");
 }
 
 // GsHooks callbacks: the same event pairs as TimingScope
@@ -216,9 +206,8 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
                              L.zero_bytes - L.off_lookback, s));
         for (int p = 0; p < L.P; ++p) {
             TimingScope ts(LABSORT_K_ONESWEEP, s);
-            // (LABSORT_OSP_JCOUNT timing builds count into hps, free once the plan is built)
             HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
-                                      counters + (size_t)p * OSP_NCTR, err, s, nullptr, LABSORT_OSP_JCOUNT ? hps : nullptr));
+                                      counters + (size_t)p * OSP_NCTR, err, s));
         }
     } else {
         HIP_TRY(launch_zero(ws, L.zero_bytes, s));
@@ -239,20 +228,12 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
     return LABSORT_OK;
 }
 
-// Merge passes after the tile sort (runs of TS_TILE keys).  KM_SORT_K = 2: the
-// pairwise merge-path pass (k_merge_pass_p); 4 or 8: K-way passes (kmerge.hip), K =
-// KM_SORT_K while that many runs remain, then the smallest power of two covering
-// the rest.
-int merge_pass_k(size_t n, size_t run) {
-    if (KM_SORT_K == 2) return 2;
-    const size_t runs = (n + run - 1) / run;
-    int k = 2;
-    while (k < KM_SORT_K && (size_t)k < runs) k <<= 1;
-    return k;
-}
+// Pairwise merge-path passes after the tile sort (runs of TS_TILE keys).  A K-way pass
+// (K = 4, 8: 5 passes instead of 13 at 2^28) was built and measured slower on MI355X
+// (9.7-14 ms vs 7.9 ms: LDS-operation bound) and removed.
 int merge_passes(size_t n) {
     int m = 0;
-    for (size_t run = TS_TILE; run < n; run *= (size_t)merge_pass_k(n, run)) ++m;
+    for (size_t run = TS_TILE; run < n; run *= 2) ++m;
     return m;
 }
 
@@ -260,7 +241,6 @@ int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char 
     const MergeLayout L = merge_layout(n);
     uint32_t *tmp = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
     uint32_t *part = reinterpret_cast<uint32_t *>(ws + L.off_part);
-    uint32_t *kmw = reinterpret_cast<uint32_t *>(ws + L.off_km);
     const int m = merge_passes(n);
     uint32_t *cur = (m % 2 == 0) ? out : tmp;
     {
@@ -270,21 +250,10 @@ int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char 
     size_t run = TS_TILE;
     for (int k = 0; k < m; ++k) {
         uint32_t *nxt = (cur == out) ? tmp : out;
-        const int K = merge_pass_k(n, run);
         TimingScope ts(LABSORT_K_MERGE, s);
-        if (KM_SORT_K == 2) {
-            HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s));
-        } else {
-            KmRuns rs{};
-            rs.explicit_runs = 0;
-            rs.K = (uint32_t)K;
-            rs.n = (uint32_t)n;
-            rs.run = (uint32_t)run;
-            rs.njobs = (uint32_t)((n + rs.K * run - 1) / (rs.K * run));
-            HIP_TRY(launch_kmerge(cur, nxt, rs, flip, kmw, s));
-        }
+        HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s));
         cur = nxt;
-        run *= (size_t)K;
+        run *= 2;
     }
     return LABSORT_OK;
 }
@@ -352,6 +321,30 @@ int resolve_algo(int algo, size_t n) {
     // merge for small arrays (fewer launches) and past the radix limit (2^30 - 1 keys)
     return n <= (size_t)LABSORT_AUTO_MERGE_MAX_KEYS || n > RADIX_MAX_N ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
 }
+// The same for key/value sorts: their radix has no fused small path (the histogram, the
+// plan and four persistent passes at every size), so merge up to its own, higher bound
+int resolve_pairs_algo(int algo, size_t n) {
+    if (algo != LABSORT_ALGO_AUTO) return algo;
+    return n <= (size_t)LABSORT_AUTO_PAIRS_MERGE_MAX_KEYS || n > RADIX_MAX_N ? LABSORT_ALGO_MERGE : LABSORT_ALGO_RADIX;
+}
+
+// Workspace of LABSORT_ALGO_RADIX at n keys: the layout of the implementation that runs,
+// and never less than the gathered layout of any smaller n, so the function is
+// monotone in n: a workspace sized for a chunk of m keys serves every shorter chunk
+// (labsort_sort_host's ragged last chunk, a rank's smaller shard) whichever
+// implementation that length selects.
+size_t radix_ws_bytes(size_t n) {
+    size_t w = radix_layout(n, 8, OSP_TILE).total;
+    if (n >= GS_MIN_N) {
+        const size_t g = gs_layout(n < GS_MAX_N ? n : GS_MAX_N - 1).total;
+        w = g > w ? g : w;
+    }
+    if (use_gather(n)) {  // LABSORT_RADIX_IMPL=gather beyond the window
+        const size_t g = gs_layout(n).total;
+        w = g > w ? g : w;
+    }
+    return w;
+}
 
 }  // namespace
 
@@ -411,6 +404,7 @@ const char *labsort_error_string(int status) {
     case LABSORT_ERR_ARG: return "invalid argument";
     case LABSORT_ERR_HIP: return "HIP runtime error";
     case LABSORT_ERR_DEVICE: return "device-side error (look-back spin limit)";
+    case LABSORT_ERR_PEER: return "another rank of the distributed sort failed";
     default: return "unknown status";
     }
 }
@@ -433,8 +427,7 @@ size_t labsort_workspace_bytes(size_t n, int algo) {
     // the implementation that will run (use_gather reads LABSORT_RADIX_IMPL; a sort run
     // after that variable changes is checked against the same function: ERR_ARG if the
     // caller's workspace was sized for the other one)
-    case LABSORT_ALGO_RADIX:
-        return use_small(n) ? sr_layout(n).total : use_gather(n) ? gs_layout(n).total : radix_layout(n, 8, OSP_TILE).total;
+    case LABSORT_ALGO_RADIX: return radix_ws_bytes(n);
     case LABSORT_ALGO_RADIX1: return radix_layout(n, 1, OS_TILE).total;
     case LABSORT_ALGO_MERGE: return merge_layout(n).total;
     default: return 0;
@@ -463,11 +456,6 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
     }
     char *ws = static_cast<char *>(d_ws);
     if (algo == LABSORT_ALGO_MERGE) return sort_merge(in, out, n, flip, ws, s);
-    if (algo == LABSORT_ALGO_RADIX && use_small(n)) {
-        TimingScope ts(LABSORT_K_SMALL, s);
-        HIP_TRY(launch_small_radix(in, out, n, flip, ws, s));
-        return LABSORT_OK;
-    }
     if (algo == LABSORT_ALGO_RADIX && use_gather(n)) {
         HookCtx hc;
         HIP_TRY(launch_gsweep_sort(in, out, n, flip, ws, s, GsHooks{&hc, hook_begin, hook_end}));
@@ -497,7 +485,7 @@ int labsort_workspace_status(const void *d_ws, size_t n, int algo, void *stream)
 }
 
 int labsort_pairs_workspace_status(const void *d_ws, size_t n, int algo, void *stream) {
-    algo = resolve_algo(algo, n);
+    algo = resolve_pairs_algo(algo, n);
     return read_status(d_ws, n > (size_t)TS_TILE_KV && algo == LABSORT_ALGO_RADIX, as_stream(stream));
 }
 
@@ -659,10 +647,7 @@ int labsort_merge(const void *d_a, size_t la, const void *d_b, size_t lb, void *
     return LABSORT_OK;
 }
 
-size_t labsort_merge_runs_workspace_bytes(size_t n) {
-    const size_t km = km_workspace_words(n) * 4, tree = align_up(n * 4, 256);  // K-way cuts | ping-pong keys
-    return km > tree ? km : tree;
-}
+size_t labsort_merge_runs_workspace_bytes(size_t n) { return align_up(n * 4, 256); }  // ping-pong keys
 
 int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, int nruns, int key_type,
                        void *d_ws, size_t ws_bytes, void *stream) {
@@ -681,8 +666,6 @@ int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, i
                                static_cast<const uint32_t *>(d_in) + h_offsets[0], n * 4, hipMemcpyDeviceToDevice, s));
         return LABSORT_OK;
     }
-    const char *impl = std::getenv("LABSORT_MERGE_RUNS");
-    if (!(impl && !std::strcmp(impl, "kway"))) {
         // log2(nruns) levels of pairwise merge-path passes over explicit pairs of runs
         // (k_merge_pass_p, one launch per pair), ping-ponging through the workspace so
         // that the last level writes d_out
@@ -717,48 +700,25 @@ int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, i
             src = dst;
         }
         return LABSORT_OK;
-    }
-    KmRuns rs{};
-    rs.explicit_runs = 1;
-    rs.K = 2;
-    while ((int)rs.K < nruns) rs.K <<= 1;
-    for (uint32_t q = 0; q <= rs.K; ++q) rs.offs[q] = (uint32_t)h_offsets[(int)q < nruns ? q : nruns];
-    rs.n = (uint32_t)h_offsets[nruns];
-    rs.njobs = 1;
-    TimingScope ts(LABSORT_K_MERGE, s);
-    HIP_TRY(launch_kmerge(static_cast<const uint32_t *>(d_in), static_cast<uint32_t *>(d_out), rs, flip_of(key_type),
-                          static_cast<uint32_t *>(d_ws), s));
-    return LABSORT_OK;
 }
 
 size_t labsort_pair_tile_keys(void) { return (size_t)TS_TILE_KV; }
 
-namespace {
-// key/value radix: the persistent onesweep passes unless LABSORT_PAIRS_OSP=0 selects
-// the non-persistent ones (8192-key look-back slots)
-bool pairs_persistent() {
-    const char *e = std::getenv("LABSORT_PAIRS_OSP");
-    return !(e && !std::strcmp(e, "0"));
-}
-size_t pairs_tile() { return pairs_persistent() ? (size_t)OSP_TILE : (size_t)OS_TILE; }
-}  // namespace
-
 size_t labsort_pairs_workspace_bytes(size_t n, int algo) {
     if (n <= (size_t)TS_TILE_KV) return 256;
-    algo = resolve_algo(algo, n);
+    algo = resolve_pairs_algo(algo, n);
     if (algo == LABSORT_ALGO_MERGE) return align_up(n * 4, 256) * 2;  // ping-pong keys | payloads
     // radix workspace | payload ping-pong
-    return align_up(radix_layout(n, 8, pairs_tile()).total, 256) + align_up(n * 4, 256);
+    return align_up(radix_layout(n, 8, OSP_TILE).total, 256) + align_up(n * 4, 256);
 }
 
 namespace {
 // 8-bit LSD radix of (key, payload) pairs: the keys' segmented histogram and plans,
 // then the persistent onesweep passes carrying each payload with its key
-// (k_onesweep_p<..., KV>), the final copy of keys and payloads under the same buffer
-// plan.  LABSORT_PAIRS_OSP=0: the non-persistent key/value pass (k_onesweep<8, ..., KV>).
+// (k_onesweep_p<true>), the final copy of keys and payloads under the same buffer plan.
 int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint32_t *vo, size_t n, uint32_t flip,
                      char *ws, hipStream_t s) {
-    const RadixLayout L = radix_layout(n, 8, pairs_tile());
+    const RadixLayout L = radix_layout(n, 8, OSP_TILE);
     Bufs b, vb;
     b.p[SEL_IN] = const_cast<uint32_t *>(ki);
     b.p[SEL_OUT] = ko;
@@ -771,36 +731,22 @@ int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint3
     uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
     uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
     Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
-    if (pairs_persistent()) {
-        HIP_TRY(launch_zero(ws, L.off_lookback, s));
-        uint32_t *hps = reinterpret_cast<uint32_t *>(ws + L.off_hps);
-        uint32_t *joint = reinterpret_cast<uint32_t *>(ws + L.off_joint);
-        SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
-        {
-            TimingScope ts(LABSORT_K_HISTOGRAM, s);
-            HIP_TRY(launch_hist_seg(ki, n, flip, hps, joint, s));
-        }
-        HIP_TRY(launch_plan8(hps, joint, n, ki == ko ? 1 : 0, plan, sps, hist, ws + L.off_lookback,
-                             L.zero_bytes - L.off_lookback, s));
-        for (int p = 0; p < L.P; ++p) {
-            TimingScope ts(LABSORT_K_ONESWEEP, s);
-            HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
-                                      counters + (size_t)p * OSP_NCTR, err, s, &vb));
-        }
-    } else {
-        HIP_TRY(launch_zero(ws, L.zero_bytes, s));
-        {
-            TimingScope ts(LABSORT_K_HISTOGRAM, s);
-            HIP_TRY(launch_histogram(ki, n, flip, 8, hist, s));
-        }
-        HIP_TRY(launch_plan(hist, n, 8, ki == ko ? 1 : 0, plan, s));
-        for (int p = 0; p < L.P; ++p) {
-            TimingScope ts(LABSORT_K_ONESWEEP, s);
-            HIP_TRY(launch_onesweep(b, plan, p, 8, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
-                                    counters + (size_t)p * OSP_NCTR, err, s, &vb));
-        }
+    HIP_TRY(launch_zero(ws, L.off_lookback, s));
+    uint32_t *hps = reinterpret_cast<uint32_t *>(ws + L.off_hps);
+    uint32_t *joint = reinterpret_cast<uint32_t *>(ws + L.off_joint);
+    SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
+    {
+        TimingScope ts(LABSORT_K_HISTOGRAM, s);
+        HIP_TRY(launch_hist_seg(ki, n, flip, hps, joint, s));
     }
-    if (!pairs_persistent() || ki == ko) {  // (persistent: as sort_radix)
+    HIP_TRY(launch_plan8(hps, joint, n, ki == ko ? 1 : 0, plan, sps, hist, ws + L.off_lookback,
+                         L.zero_bytes - L.off_lookback, s));
+    for (int p = 0; p < L.P; ++p) {
+        TimingScope ts(LABSORT_K_ONESWEEP, s);
+        HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
+                                  counters + (size_t)p * OSP_NCTR, err, s, &vb));
+    }
+    if (ki == ko) {  // (out of place: pass 0's launch copies an all-constant input)
         HIP_TRY(launch_final_copy(b, plan, n, s));
         HIP_TRY(launch_final_copy(vb, plan, n, s));
     }
@@ -814,7 +760,7 @@ int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void
     if (!d_keys_in || !d_vals_in || !d_keys_out || !d_vals_out) return LABSORT_ERR_ARG;
     if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
     if (algo != LABSORT_ALGO_RADIX && algo != LABSORT_ALGO_MERGE && algo != LABSORT_ALGO_AUTO) return LABSORT_ERR_ARG;
-    algo = resolve_algo(algo, n);
+    algo = resolve_pairs_algo(algo, n);
     if (n > (algo == LABSORT_ALGO_MERGE ? (size_t)0x7FFFFFFFu : RADIX_MAX_N)) return LABSORT_ERR_ARG;
     // in place only as a whole: one side aliased and the other not would read
     // payloads that the key side's passes already overwrote
@@ -877,6 +823,14 @@ int labsort_upper_bound(const void *d_sorted, size_t n, int key_type, const uint
     if (key_type != LABSORT_KEY_U32 && key_type != LABSORT_KEY_I32) return LABSORT_ERR_ARG;
     HIP_TRY(launch_upper_bound(static_cast<const uint32_t *>(d_sorted), n, flip_of(key_type), d_values, nv, d_out,
                                as_stream(stream)));
+    return LABSORT_OK;
+}
+
+int labsort_copy(const void *d_in, void *d_out, size_t n, void *stream) {
+    if (n == 0) return LABSORT_OK;
+    if (!d_in || !d_out) return LABSORT_ERR_ARG;
+    TimingScope ts(LABSORT_K_COPY, as_stream(stream));
+    HIP_TRY(launch_stream_copy(static_cast<const uint32_t *>(d_in), static_cast<uint32_t *>(d_out), n, as_stream(stream)));
     return LABSORT_OK;
 }
 

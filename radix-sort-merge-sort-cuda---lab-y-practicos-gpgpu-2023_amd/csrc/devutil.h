@@ -18,7 +18,7 @@ __device__ __forceinline__ void st_agent(uint32_t *p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Streamed key loads (LABSORT_NT_LOADS, one bit per kernel family, NT_*): a pass reads
+// Streamed key loads (NT_LOADS, one bit per kernel family, NT_*): a pass reads
 // each key once, so its loads are issued nontemporal and the L2 keeps its capacity for
 // the lines being written.  For the onesweep scatter that matters: the partial 64-B
 // granules two consecutive tiles write at a digit-run boundary meet in the L2 before
@@ -26,12 +26,12 @@ __device__ __forceinline__ void st_agent(uint32_t *p, uint32_t v) {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 template <int BIT>
 __device__ __forceinline__ uint32_t ld_stream(const uint32_t *p) {
-    if constexpr ((LABSORT_NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
+    if constexpr ((NT_LOADS & BIT) != 0) return __builtin_nontemporal_load(p);
     else return *p;
 }
 template <int BIT>
 __device__ __forceinline__ uint4 ld_stream4(const uint4 *p) {
-    if constexpr ((LABSORT_NT_LOADS & BIT) != 0) {
+    if constexpr ((NT_LOADS & BIT) != 0) {
         const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
         return make_uint4(v.x, v.y, v.z, v.w);
     } else {
@@ -100,17 +100,12 @@ __device__ __forceinline__ bool lds_lane_ordered(uint32_t *scratch, uint32_t lan
 // whole wave shares (sorted or nearly sorted input: the high digits of 64 consecutive
 // keys) takes one add of 64 instead of 64 adds serialised on one address.  All 64
 // lanes active.
-#ifndef LABSORT_RANK_UNIFORM
-#define LABSORT_RANK_UNIFORM 1
-#endif
 __device__ __forceinline__ uint32_t wave_atomic_rank(uint32_t *wh, uint32_t d, uint32_t lane) {
-    if (LABSORT_RANK_UNIFORM) {
-        const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-        if (__ballot(d != d0) == 0ull) {
-            uint32_t b = 0;
-            if (lane == 0) b = __hip_atomic_fetch_add(wh + d0, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-            return __builtin_amdgcn_readfirstlane(b) + lane;
-        }
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    if (__ballot(d != d0) == 0ull) {
+        uint32_t b = 0;
+        if (lane == 0) b = __hip_atomic_fetch_add(wh + d0, 64u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+        return __builtin_amdgcn_readfirstlane(b) + lane;
     }
     return __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }

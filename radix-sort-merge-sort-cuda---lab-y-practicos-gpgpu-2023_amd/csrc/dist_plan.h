@@ -25,7 +25,10 @@
 //      and holds the contiguous range [goff, goff + total) of the sorted array.
 #pragma once
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
+
+#include <chrono>
 
 #include <algorithm>
 #include <vector>
@@ -104,15 +107,45 @@ inline int rank_cuts(int r, uint64_t m, const std::vector<Splitter> &spl, const 
     return LABSORT_OK;
 }
 
+// Collectives of one sort_rank call, in order (the timing records index them)
+enum Coll { C_SAMPLES = 0, C_COUNTS, C_GROW, C_NCOLL };
+
 struct Result {
     const uint32_t *data = nullptr;  // this rank's sorted range (owned by the rank operations)
     uint64_t count = 0;              // keys in it
     uint64_t goff = 0;               // its offset in the global sorted array
     uint64_t sent = 0;               // key bytes this rank sent to its peers
+    // host wall clock, ms since the call started: arrival at / return from each collective
+    // (C_GROW runs only when some rank's range outgrew the pre-sized receive buffer; -1
+    // when it did not run).  leave - arrive = time spent waiting for the slowest peer
+    // (plus the collective's own latency); the rest of the plan phase is this rank's work.
+    double arrive[C_NCOLL] = {-1.0, -1.0, -1.0}, leave[C_NCOLL] = {-1.0, -1.0, -1.0};
+    int failed_rank = -1;  // the lowest rank that reported a failure (-1: none)
 };
 
 // Phase marks the schedule reports to the rank operations (timing hooks)
 enum Mark { M_START = 0, M_SORTED, M_PLANNED, M_EXCHANGED, M_MERGED, M_NMARKS };
+
+// Test hook (LABSORT_TEST_FAIL=<phase>:<rank>, phase local_sort | bounds | recv): the
+// named rank reports a failure at that step, as an out-of-memory or an expired device
+// spin would; the tests check that every rank then returns an error instead of waiting
+// for the failed one.
+inline int injected_failure(const char *phase, int r) {
+    const char *e = getenv("LABSORT_TEST_FAIL");
+    if (!e) return LABSORT_OK;
+    const char *c = strchr(e, ':');
+    if (!c || (size_t)(c - e) != strlen(phase) || strncmp(e, phase, (size_t)(c - e)) != 0) return LABSORT_OK;
+    return atoi(c + 1) == r ? LABSORT_ERR_DEVICE : LABSORT_OK;
+}
+
+// Receive buffer sized before the counts are known: every range lies within about
+// m / (256 p) keys of n / p (samples_per_rank), so 1.25 n / p (+ 64 Ki keys) covers it
+// unless the communicator is broken; a rank whose range is larger grows its buffer in an
+// extra status round that every rank takes part in (all ranks see all the counts).
+inline uint64_t recv_estimate(uint64_t total, int p) {
+    const uint64_t share = (total + (uint64_t)p - 1) / (uint64_t)p;
+    return share + share / 4 + ((uint64_t)1 << 16);
+}
 
 // One rank of the distributed sort.
 //   Ops  (rank operations, on the rank's device or on the host):
@@ -120,7 +153,7 @@ enum Mark { M_START = 0, M_SORTED, M_PLANNED, M_EXCHANGED, M_MERGED, M_NMARKS };
 //     int sample(const uint32_t *sorted, uint64_t m, size_t s, uint32_t *h_out)       (blocking)
 //     int bounds(const uint32_t *sorted, uint64_t m, const uint32_t *h_vals, size_t nv,
 //                uint32_t *h_out)                                                     (blocking)
-//     int recv_buffer(uint64_t total, uint32_t **recv)
+//     int recv_buffer(uint64_t total, uint32_t **recv)      -- grows, never shrinks
 //     int copy_local(uint32_t *dst, const uint32_t *src, uint64_t count)
 //     int merge(const uint32_t *recv, const uint64_t *offs, int p, uint32_t *h_sink,
 //               const uint32_t **result)   -- h_sink: also copy the result to this host address
@@ -132,54 +165,109 @@ enum Mark { M_START = 0, M_SORTED, M_PLANNED, M_EXCHANGED, M_MERGED, M_NMARKS };
 //                  uint32_t *const *recv, const uint64_t *rcount)   -- self pieces excluded
 // `h_out_base` (nullable): the caller's host array of the whole sorted output; this
 // rank's range is copied to h_out_base + goff.
+//
+// Failures: a rank whose own step fails (local sort, samples, bounds, buffers) still takes
+// part in every collective up to the exchange and reports its status word in the record;
+// after each allgather every rank checks all status words and, if any is set, returns --
+// its own error, or LABSORT_ERR_PEER when only another rank failed -- so no rank is left
+// waiting in a collective for a rank that gave up.  A communicator whose collective itself
+// fails returns that failure at once.
 template <class Ops, class Comm>
 int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t flip, uint32_t *h_out_base,
               Result &res) {
     const int p = comm.size(), r = comm.rank();
-    int st;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto now_ms = [&]() {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    };
+    res = Result{};
+    // one collective with every rank's status word at offset 0 of its record
+    auto gather = [&](int k, const std::vector<uint8_t> &mine, std::vector<uint8_t> &all, int &st) {
+        res.arrive[k] = now_ms();
+        const int c = comm.allgather(mine.data(), all.data(), mine.size());
+        res.leave[k] = now_ms();
+        if (c) return c;  // the communicator failed: nothing was agreed
+        for (int i = 0; i < p; ++i) {
+            uint32_t w;
+            memcpy(&w, all.data() + (size_t)i * mine.size(), 4);
+            if (w && res.failed_rank < 0) res.failed_rank = i;
+        }
+        if (res.failed_rank >= 0) return st ? st : LABSORT_ERR_PEER;
+        return LABSORT_OK;
+    };
     ops.mark(M_START);
     const uint32_t *S = nullptr;
-    if ((st = ops.local_sort(in, m, &S))) return st;
+    int st = injected_failure("local_sort", r);
+    if (!st) st = ops.local_sort(in, m, &S);
     ops.mark(M_SORTED);
-    res = Result{};
-    // (one rank runs the whole schedule too: its communicator is exercised, at the
-    // price of one copy of the shard)
-    // 2. shard sizes and samples of every rank
-    const size_t s = samples_per_rank(p), rec = 8 + 4 * s;
+    // 2. status, shard size and samples of every rank
+    const size_t s = samples_per_rank(p), rec = 16 + 4 * s;
     std::vector<uint8_t> mine(rec, 0), all(rec * (size_t)p, 0);
-    memcpy(mine.data(), &m, 8);
-    if (m && (st = ops.sample(S, m, s, reinterpret_cast<uint32_t *>(mine.data() + 8)))) return st;
-    if ((st = comm.allgather(mine.data(), all.data(), rec))) return st;
+    if (!st && m) st = ops.sample(S, m, s, reinterpret_cast<uint32_t *>(mine.data() + 16));
+    uint32_t sw = (uint32_t)st;
+    memcpy(mine.data(), &sw, 4);
+    memcpy(mine.data() + 8, &m, 8);
+    if (int c = gather(C_SAMPLES, mine, all, st)) return c;
     std::vector<uint64_t> ms(p);
     std::vector<uint32_t> samples((size_t)p * s);
+    uint64_t ntot = 0;
     for (int i = 0; i < p; ++i) {
-        memcpy(&ms[i], all.data() + (size_t)i * rec, 8);
-        memcpy(&samples[(size_t)i * s], all.data() + (size_t)i * rec + 8, 4 * s);
+        memcpy(&ms[i], all.data() + (size_t)i * rec + 8, 8);
+        memcpy(&samples[(size_t)i * s], all.data() + (size_t)i * rec + 16, 4 * s);
+        ntot += ms[i];
     }
-    if (ms[r] != m) return LABSORT_ERR_ARG;  // the communicator mixed up the ranks
-    // 3-4. splitters (the same on every rank) and this rank's cut points
+    if (ms[r] != m) st = LABSORT_ERR_ARG;  // the communicator mixed up the ranks
+    // 3-4. splitters (the same on every rank) and this rank's cut points; the receive
+    // buffer pre-sized
     const std::vector<Splitter> spl = choose_splitters(p, ms.data(), samples.data(), s, flip);
     const std::vector<uint32_t> vals = plan_values(spl, p, flip);
     std::vector<uint32_t> ub(vals.size(), 0u);
-    if (m && (st = ops.bounds(S, m, vals.data(), vals.size(), ub.data()))) return st;
-    std::vector<uint64_t> cut(p + 1);
-    if ((st = rank_cuts(r, m, spl, ub.data(), p, cut.data()))) return st;
-    // 5. piece counts of every rank: C[i * p + j] = keys rank i sends to rank j
-    std::vector<uint64_t> sc(p), C((size_t)p * p);
-    for (int j = 0; j < p; ++j) sc[j] = cut[j + 1] - cut[j];
-    if ((st = comm.allgather(sc.data(), C.data(), 8 * (size_t)p))) return st;
-    for (int j = 0; j < p; ++j)
-        if (C[(size_t)r * p + j] != sc[j]) return LABSORT_ERR_ARG;
+    std::vector<uint64_t> cut(p + 1, 0);
+    if (!st) st = injected_failure("bounds", r);
+    if (!st && m) st = ops.bounds(S, m, vals.data(), vals.size(), ub.data());
+    if (!st) st = rank_cuts(r, m, spl, ub.data(), p, cut.data());
+    const uint64_t est = recv_estimate(ntot, p);
+    uint32_t *R = nullptr;
+    if (!st) st = injected_failure("recv", r);
+    if (!st) st = ops.recv_buffer(est, &R);
+    // 5. status and piece counts of every rank: C[i * p + j] = keys rank i sends to rank j
+    std::vector<uint64_t> sc(p, 0), C((size_t)p * p);
+    for (int j = 0; j < p && !st; ++j) sc[j] = cut[j + 1] - cut[j];
+    {
+        std::vector<uint8_t> cm(8 * ((size_t)p + 1), 0), ca(cm.size() * (size_t)p, 0);
+        sw = (uint32_t)st;
+        memcpy(cm.data(), &sw, 4);
+        memcpy(cm.data() + 8, sc.data(), 8 * (size_t)p);
+        if (int c = gather(C_COUNTS, cm, ca, st)) return c;
+        for (int i = 0; i < p; ++i) memcpy(&C[(size_t)i * p], ca.data() + (size_t)i * cm.size() + 8, 8 * (size_t)p);
+    }
+    // every row must add up to its rank's shard: a check all ranks reach the same verdict on
+    uint64_t rmax = 0;
+    for (int i = 0; i < p; ++i) {
+        uint64_t row = 0, col = 0;
+        for (int j = 0; j < p; ++j) {
+            row += C[(size_t)i * p + j];
+            col += C[(size_t)j * p + i];
+        }
+        if (row != ms[i]) return LABSORT_ERR_ARG;
+        rmax = col > rmax ? col : rmax;
+    }
     std::vector<uint64_t> roff(p + 1, 0);
     for (int i = 0; i < p; ++i) roff[i + 1] = roff[i] + C[(size_t)i * p + r];
     uint64_t goff = 0;
     for (int i = 0; i < p; ++i)
         for (int j = 0; j < r; ++j) goff += C[(size_t)i * p + j];
     const uint64_t total = roff[p];
+    if (rmax > est) {  // some range outgrew the pre-sized buffers: grow, then agree again
+        st = ops.recv_buffer(total, &R);
+        std::vector<uint8_t> gm(8, 0), ga(8 * (size_t)p, 0);
+        sw = (uint32_t)st;
+        memcpy(gm.data(), &sw, 4);
+        if (int c = gather(C_GROW, gm, ga, st)) return c;
+    } else if ((st = ops.recv_buffer(total, &R))) {
+        return st;  // (cannot allocate: total <= est was allocated above)
+    }
     ops.mark(M_PLANNED);
-    uint32_t *R = nullptr;
-    if ((st = ops.recv_buffer(total, &R))) return st;
-    if (sc[r] && (st = ops.copy_local(R + roff[r], S + cut[r], sc[r]))) return st;
     std::vector<const uint32_t *> sp(p, nullptr);
     std::vector<uint32_t *> rp(p, nullptr);
     std::vector<uint64_t> scount(p, 0), rcount(p, 0);
@@ -193,6 +281,8 @@ int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t fli
         sent += 4 * sc[j];
     }
     if ((st = comm.exchange(sp.data(), scount.data(), rp.data(), rcount.data()))) return st;
+    // (the own piece after the exchange: nothing can fail between the agreement and it)
+    if (sc[r] && (st = ops.copy_local(R + roff[r], S + cut[r], sc[r]))) return st;
     ops.mark(M_EXCHANGED);
     // 6. merge of the p received runs in rank order
     const uint32_t *out = nullptr;

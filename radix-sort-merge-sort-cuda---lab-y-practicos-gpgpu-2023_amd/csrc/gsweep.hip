@@ -43,12 +43,9 @@ namespace labsort {
 namespace {
 
 constexpr int GB = GS_BLOCK, GK = GS_KPT, GT = GS_TILE, GW = GS_BLOCK / WAVE;
-#ifndef LABSORT_GS_WPE
-#define LABSORT_GS_WPE (GS_KPT > 16 ? 2 : 3)
-#endif
 // launch bounds: at least this many waves per SIMD (a VGPR cap).  k_gsweep needs 77
 // VGPRs, k_gcopy 54, so 6 waves per SIMD fit: 3 workgroups of 512 per CU.
-constexpr int GS_WAVES_PER_EU = LABSORT_GS_WPE;
+constexpr int GS_WAVES_PER_EU = 3;
 static_assert(GT == GB * GK && GW * WAVE == GB, "tile shape");
 
 struct GsTables {
@@ -303,7 +300,7 @@ __device__ __forceinline__ uint32_t gs_fused_prologue(const uint32_t *acc, int p
     return h ? 0u : c + part[d];
 }
 
-// Pass 1 when no memset ran (LABSORT_GS_FUSED=2): pass 0 accumulated nothing, so the
+// Pass 1 of the fused path (no memset runs): pass 0 accumulated nothing, so the
 // digit min / max come from its per-tile pairs and the totals from its 128 tile rows
 // (every workgroup sums them: 128 KB from L2), and workgroup 0 publishes the min / max
 // in line 0 of the min / max lines for the passes after it.  part: 288 words.
@@ -779,25 +776,17 @@ __global__ __launch_bounds__(256) void k_gsum(const uint32_t *__restrict__ rt, c
     }
 }
 
-// k_gout: the tables of this pass's output buffer, G tiles per workgroup (4 threads
-// per digit, G/4 tiles each); digit-major writes go through LDS so each is a line
-// segment.  SMALL (at most GS_SMALL_NG scan groups of GS_GROUP tiles): 16-tile
-// workgroups that sum the earlier tiles' and all tiles' counts themselves from the tile
-// rows, so k_gsum is not launched (one scan launch instead of two; at 2^20 keys the
-// launches and latency chains, not the bytes, set the time).  Workgroup 0 writes the
-// sentinel and, after pass 0, the digit min / max.
-constexpr int GS_SGROUP = 16;  // tiles per workgroup of the SMALL scan
-template <bool SMALL>
+// k_gout: the tables of this pass's output buffer, GS_GROUP tiles per workgroup (4
+// threads per digit, 16 tiles each); digit-major writes go through LDS so each is a line
+// segment.  Workgroup 0 writes the sentinel and, after pass 0, the digit min / max.
 __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, const uint32_t *__restrict__ gsx,
-                                               const uint32_t *__restrict__ tot, const uint32_t *__restrict__ mm,
-                                               const uint32_t *__restrict__ gmm,
+                                               const uint32_t *__restrict__ tot, const uint32_t *__restrict__ gmm,
                                                GsTables tA, GsTables tB, GsState *st, int pass, uint32_t ntp,
                                                uint32_t n) {
     if (!gs_active(st, pass)) return;
-    constexpr int G = SMALL ? GS_SGROUP : GS_GROUP, TPQ = G / 4;
+    constexpr int G = GS_GROUP, TPQ = G / 4;
     __shared__ uint32_t lsb[G][257], srb[G][257];
     __shared__ uint32_t part[4][256];
-    __shared__ uint32_t pre[2][4][256];
     __shared__ uint32_t wsum[16];
     __shared__ uint32_t red[16][2];
     const GsTables tb = gs_dst(st, pass) == 1u ? tA : tB;
@@ -810,32 +799,11 @@ __global__ __launch_bounds__(1024) void k_gout(const uint32_t *__restrict__ rt, 
         h += w[i] >> 16;
     }
     part[q][d] = h;
-    uint32_t total = 0, before = 0;
-    if constexpr (SMALL) {
-        // counts of digit d in the tiles before this workgroup's and in all tiles
-        uint32_t sb = 0, sa = 0;
-#pragma unroll 8
-        for (uint32_t t = q; t < ntp; t += 4u) {
-            const uint32_t c = rt[(size_t)t * 256 + d] >> 16;
-            sa += c;
-            sb += t < g * (uint32_t)G ? c : 0u;
-        }
-        pre[0][q][d] = sb;
-        pre[1][q][d] = sa;
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            before += pre[0][r][d];
-            total += pre[1][r][d];
-        }
-    } else {
-        total = tot[d];
-        before = gsx[(size_t)(g * G / GS_GROUP) * 256 + d];
-    }
+    const uint32_t total = tot[d], before = gsx[(size_t)g * 256 + d];
     if (g == 0) {
         if (tid == 0) tb.ls[(size_t)256 * ntp] = n;  // sentinel start after the last run
-        if (pass == 0)  // per tile (SMALL) or per scan group: packed digit min / max pairs
-            gs_reduce_minmax<1024>(SMALL ? mm : gmm, SMALL ? ntp : (ntp + GS_GROUP - 1) / GS_GROUP, red, st);
+        if (pass == 0)  // per scan group: packed digit min / max pairs
+            gs_reduce_minmax<1024>(gmm, (ntp + GS_GROUP - 1) / GS_GROUP, red, st);
     }
     // global exclusive digit offsets from the digit totals
     const uint32_t gx = block_excl_scan<1024, 256>(q == 0 ? total : 0u, wsum);
@@ -903,15 +871,6 @@ __global__ __launch_bounds__(GB, GS_WAVES_PER_EU) void k_gcopy(const uint32_t *_
 
 inline size_t al(size_t x) { return (x + 65535) / 65536 * 65536; }
 
-// LABSORT_GS_FUSED: 0 keeps the scan launches at every size (A/B); 1 clears the
-// accumulators with a memset launch; 2 has pass 0 clear those of passes 1-3 and pass 1
-// read pass 0's rows and pairs
-int gs_fused(uint32_t ng) {
-    const char *e = std::getenv("LABSORT_GS_FUSED");
-    if (ng > (uint32_t)GS_SMALL_NG || (e && e[0] == '0')) return 0;
-    return (e && e[0] == '1') ? 1 : 2;
-}
-
 }  // namespace
 
 // ---- host side -------------------------------------------------------------------------
@@ -968,13 +927,11 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
     uint32_t *rt2 = reinterpret_cast<uint32_t *>(ws + L.off_rt2);
     const unsigned grid = 8u * ((ntp + 7u) / 8u);
     hipError_t e;
-    if (const int fz = gs_fused(ng)) {  // sweeps 0-3, the gathered copy (+ a memset: fz = 1)
+    if (ng <= (uint32_t)GS_SMALL_NG) {  // fused small path: sweeps 0-3 and the gathered copy, no memset
         uint32_t *acc = flags;
-        if (fz == 1 && (e = launch_zero(ws + L.off_state, 512 + GS_FWORDS * 4, s)) != hipSuccess) return e;
         for (int p = 0; p < 4; ++p) {
             if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GSWEEP, s);
-            k_gsweep<true><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, acc, p, (uint32_t)n, ntp, flip,
-                                               fz == 2);
+            k_gsweep<true><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, acc, p, (uint32_t)n, ntp, flip, 1);
             if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
             if ((e = hipGetLastError()) != hipSuccess) return e;
         }
@@ -983,20 +940,15 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
         if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GCOPY, s);
         return hipGetLastError();
     }
-    e = launch_zero(ws + L.off_state, 512 + (ng > (uint32_t)GS_SMALL_NG ? (size_t)4 * ng * 256 * 4 : 0), s);
+    e = launch_zero(ws + L.off_state, 512 + (size_t)4 * ng * 256 * 4, s);
     if (e != hipSuccess) return e;
     for (int p = 0; p < 4; ++p) {
         if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GSWEEP, s);
         k_gsweep<false><<<grid, GB, 0, s>>>(in, A, B, t[0], t[1], rt, rt2, mm, st, flags, p, (uint32_t)n, ntp, flip, 0);
         if (hooks.end) hooks.end(hooks.ctx, LABSORT_K_GSWEEP, s);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        if (ng <= (uint32_t)GS_SMALL_NG) {
-            k_gout<true><<<(ntp + GS_SGROUP - 1) / GS_SGROUP, 1024, 0, s>>>(rt, gsx, gx, mm, gmm, t[0], t[1], st, p,
-                                                                           ntp, (uint32_t)n);
-        } else {
-            k_gsum<<<ng, 256, 0, s>>>(rt, mm, gsx, gx, gmm, flags, st, p, ntp, ng);
-            k_gout<false><<<ng, 1024, 0, s>>>(rt, gsx, gx, mm, gmm, t[0], t[1], st, p, ntp, (uint32_t)n);
-        }
+        k_gsum<<<ng, 256, 0, s>>>(rt, mm, gsx, gx, gmm, flags, st, p, ntp, ng);
+        k_gout<<<ng, 1024, 0, s>>>(rt, gsx, gx, gmm, t[0], t[1], st, p, ntp, (uint32_t)n);
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     if (hooks.begin) hooks.begin(hooks.ctx, LABSORT_K_GCOPY, s);

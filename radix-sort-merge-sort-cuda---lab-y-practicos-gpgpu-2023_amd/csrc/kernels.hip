@@ -220,9 +220,6 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) atomicAdd(&h[(k[j] & 255u) * SL + slot], 1u);
-#ifdef LABSORT_HS_DIAG_NOJOINT
-        return;  // diagnostic timing build: digit 0 only (results invalid)
-#endif
         if (__ballot(fld(k[0], 2) == fld(k[3], 2)) == 0ull) {  // no repeats here
 #pragma unroll
             for (int p = 0; p < 3; ++p)
@@ -307,9 +304,9 @@ __global__ __launch_bounds__(HIST_BLOCK) void k_hist_seg(const uint32_t *__restr
         if (c) atomicAdd(&hps[seg * 256 + i], c);
     }
     // field f = (digit p+1) << 4 | (top nibble of digit p) -> joint[p+1][nibble][digit].
-    // Each workgroup starts its flush at a different place (HS_ROT), so the ~12 K
+    // Each workgroup starts its flush at a different place, so the ~12 K
     // atomics of workgroups that finish together do not queue on the same lines.
-    const uint32_t rot = HS_ROT ? (blockIdx.x * (uint32_t)HIST_BLOCK) % (3u * JF) : 0u;
+    const uint32_t rot = (blockIdx.x * (uint32_t)HIST_BLOCK) % (3u * JF);
     for (int i0 = threadIdx.x; i0 < 3 * JF; i0 += HIST_BLOCK) {
         int i = i0 + (int)rot;
         i = i >= 3 * JF ? i - 3 * JF : i;
@@ -369,7 +366,7 @@ __device__ void build_segplan(SegPlan *__restrict__ sp, const uint32_t *__restri
 // previous digit's top nibble (starts from its histogram), histograms = the joint
 // counts k_hist_seg wrote; one chain when the previous active digit is not q - 1.
 // 256 threads; hist: the 4 digit histograms; sh, start: LDS scratch.
-__device__ void build_segplan_later(SegPlan *__restrict__ sps, int q, uint32_t prev, uint32_t n, int seg_later,
+__device__ void build_segplan_later(SegPlan *__restrict__ out, int q, uint32_t prev, uint32_t n, int seg_later,
                                     const uint32_t *hist, const uint32_t *__restrict__ joint, uint32_t *sh,
                                     uint32_t *start) {
     const uint32_t t = threadIdx.x, lane = t & 63u, wid = t >> 6;
@@ -377,7 +374,7 @@ __device__ void build_segplan_later(SegPlan *__restrict__ sps, int q, uint32_t p
         for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[q * 256 + t];
         if (t <= (uint32_t)NSEG) start[t] = t ? n : 0u;
         __syncthreads();
-        build_segplan(sps + q, sh, start, 2u, sh);
+        build_segplan(out, sh, start, 2u, sh);
         return;
     }
     // segment starts: exclusive prefix over nibble groups of hist[prev]
@@ -395,7 +392,7 @@ __device__ void build_segplan_later(SegPlan *__restrict__ sps, int q, uint32_t p
     if ((t & 15u) == 0) start[t >> 4] = x + add - v;
     if (t == 0) start[NSEG] = n;
     __syncthreads();
-    build_segplan(sps + q, joint + (size_t)q * NSEG * 256, start, 1u, sh);
+    build_segplan(out, joint + (size_t)q * NSEG * 256, start, 1u, sh);
 }
 
 // Pass plan for the 8-bit radix (as k_plan: totals, trivial passes, ping-pong
@@ -446,6 +443,7 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
             plan->dst[p] = SEL_SKIP;
             plan->next[p] = NEXT_NONE;
             plan->prev[p] = NEXT_NONE;
+            plan->digit[p] = (uint32_t)p;
         }
         for (int p = 0; p < 4; ++p) {
             prevs[p] = NEXT_NONE;
@@ -495,7 +493,78 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
     for (int q = first + 1; q < 4; ++q) {
         if (prevs[q] == NEXT_NONE) continue;  // (block-uniform)
         __syncthreads();  // sh, start reused
-        build_segplan_later(sps, q, prevs[q], n, seg_later, hist, joint, sh, start);
+        build_segplan_later(sps + q, q, prevs[q], n, seg_later, hist, joint, sh, start);
+    }
+}
+
+// Plan of the local-pass path (lsweep.hip): the local pass has sorted every tile by
+// digit 0 (its logical order is digit-0 order), so the launches that follow sort by the
+// active digits among 1..3: launch j by digit[j], reading TMP (the local pass's output,
+// gathered through the run tables) for j = 0 and the previous launch's output after it,
+// the last one writing OUT (TMP2 and TMP in between, so a launch never reads the buffer it
+// writes, in place or not).  With no active digit the logical order is the sorted array
+// and k_lcopy gathers it into OUT (copy_from = TMP).  Segments: as in k_plan8, with the
+// local pass's digit 0 as the previous digit of launch 0.  hist_out: the 4 digit
+// histograms (digit 0 = tot0, digits 1-3 = the joint marginals).  Workgroups 1.. clear the
+// look-back region (zp, zn4 uint4s) meanwhile.
+__global__ __launch_bounds__(256) void k_plan_l(const uint32_t *__restrict__ tot0, const uint32_t *__restrict__ joint,
+                                                uint32_t n, Plan *__restrict__ plan, SegPlan *__restrict__ sps,
+                                                uint32_t *__restrict__ hist_out, uint4 *__restrict__ zp, size_t zn4) {
+    if (blockIdx.x > 0) {
+        const size_t stride = (size_t)(gridDim.x - 1) * blockDim.x;
+        for (size_t i = (size_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < zn4; i += stride)
+            zp[i] = make_uint4(0u, 0u, 0u, 0u);
+        return;
+    }
+    __shared__ uint32_t hist[4 * 256];
+    __shared__ uint32_t sh[NSEG * 256 + 8];
+    __shared__ uint32_t start[NSEG + 1];
+    __shared__ uint32_t triv[4], act[3], nact;
+    const uint32_t t = threadIdx.x;
+    if (t < 4) triv[t] = 0;
+    __syncthreads();
+    uint32_t v[4] = {tot0[t], 0u, 0u, 0u};
+    for (int s = 0; s < NSEG; ++s) {
+#pragma unroll
+        for (int p = 1; p < 4; ++p) v[p] += joint[(p * NSEG + s) * 256 + t];  // marginal over the nibble
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        hist[p * 256 + t] = v[p];
+        hist_out[p * 256 + t] = v[p];
+        if (v[p] == n) triv[p] = 1;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t k = 0;
+        for (int p = 1; p < 4; ++p)
+            if (!triv[p]) act[k++] = (uint32_t)p;
+        nact = k;
+        for (int j = 0; j < MAX_PASSES; ++j) {
+            plan->src[j] = SEL_SKIP;
+            plan->dst[j] = SEL_SKIP;
+            plan->next[j] = NEXT_NONE;
+            plan->prev[j] = NEXT_NONE;
+            plan->digit[j] = 0;
+        }
+        uint32_t src = SEL_TMP;
+        for (uint32_t j = 0; j < k; ++j) {
+            const uint32_t dst = j + 1 == k ? SEL_OUT : (j % 2 == 0 ? SEL_TMP2 : SEL_TMP);
+            plan->src[j] = src;
+            plan->dst[j] = dst;
+            plan->digit[j] = act[j];
+            plan->prev[j] = j ? act[j - 1] : 0u;
+            plan->next[j] = j + 1 < k ? act[j + 1] : NEXT_NONE;
+            src = dst;
+        }
+        plan->active = k;
+        plan->copy_from = k ? SEL_SKIP : SEL_TMP;
+    }
+    __syncthreads();
+    const uint32_t k = nact;
+    for (uint32_t j = 0; j < k; ++j) {
+        __syncthreads();  // sh, start reused
+        build_segplan_later(sps + j, (int)act[j], j ? act[j - 1] : 0u, n, 1, hist, joint, sh, start);
     }
 }
 
@@ -523,16 +592,12 @@ __global__ __launch_bounds__(256) void k_final_copy(Bufs b, const Plan *__restri
 // wave's stores to slots 64 apart (one per digit: sorted or strided input, where every
 // digit of a tile has the same count) spread over the banks instead of all landing on
 // one, and the slot-order read-back stays conflict-free.
-#ifndef LABSORT_OSP_PAD
-#define LABSORT_OSP_PAD 1
-#endif
-__device__ __forceinline__ uint32_t osp_pad(uint32_t i) { return LABSORT_OSP_PAD ? i + (i >> 5) : i; }
+__device__ __forceinline__ uint32_t osp_pad(uint32_t i) { return i + (i >> 5); }
 
-template <int BITS, int BLOCK, int KPT, bool KV = false>
+template <int BITS, int BLOCK, int KPT>
 struct OsSmem {
     static constexpr int R = 1 << BITS, W = BLOCK / WAVE, TILE = BLOCK * KPT;
     uint32_t keys[TILE + TILE / 32];  // padded (osp_pad)
-    uint32_t vals[KV ? TILE + TILE / 32 : 1];  // key/value: payloads reordered with their keys
     uint32_t whist[W * R];
     uint32_t gscan[R];
     uint32_t dstart[R];
@@ -542,17 +607,12 @@ struct OsSmem {
     uint32_t tile;
 };
 
-constexpr uint32_t SPIN_LIMIT = 1u << 22;
-
-// KV: key/value pairs; vbufs holds the payload buffers (IN, OUT, TMP) that the plan
-// selects exactly as for the keys, and each payload is reordered and scattered with
-// its key (stable, like the keys).
-template <int BITS, int BLOCK, int KPT, bool KV = false>
+// (LABSORT_ALGO_RADIX1: letra.pdf's literal 1-bit passes, BITS = 1)
+template <int BITS, int BLOCK, int KPT>
 __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n,
                                                     uint32_t flip, const uint32_t *__restrict__ ghist,
-                                                    uint32_t *lookback, uint32_t *counter, uint32_t *err,
-                                                    Bufs vbufs) {
-    using S = OsSmem<BITS, BLOCK, KPT, KV>;
+                                                    uint32_t *lookback, uint32_t *counter, uint32_t *err) {
+    using S = OsSmem<BITS, BLOCK, KPT>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE;
     constexpr uint32_t RM = R - 1;
     static_assert(R <= BLOCK, "one thread per digit");
@@ -589,15 +649,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
             k[j] = idx < n ? ld_stream<NT_OS>(in + idx) : sentinel;
         }
     }
-    uint32_t v[KV ? KPT : 1];
-    if constexpr (KV) {
-        const uint32_t *__restrict__ vin = vbufs.p[srcsel];
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t idx = wbase + j * WAVE;
-            v[j] = idx < n ? vin[idx] : 0u;
-        }
-    }
     uint32_t dig[KPT], rank[KPT];
 #pragma unroll
     for (int j = 0; j < KPT; ++j) dig[j] = ((k[j] ^ flip) >> shift) & RM;
@@ -627,7 +678,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
     for (int j = 0; j < KPT; ++j) {
         const uint32_t pos = osp_pad(sm.dstart[dig[j]] + wh[dig[j]] + rank[j]);
         sm.keys[pos] = k[j];
-        if constexpr (KV) sm.vals[pos] = v[j];
     }
 
     // decoupled look-back: exclusive count of my digit in all earlier tiles
@@ -663,7 +713,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
             const uint32_t key = sm.keys[osp_pad(i)];
             const uint32_t d = ((key ^ flip) >> shift) & RM;
             out[sm.delta[d] + i] = key;
-            if constexpr (KV) vbufs.p[plan->dst[pass]][sm.delta[d] + i] = sm.vals[osp_pad(i)];
         }
     }
 }
@@ -671,199 +720,198 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
 // ---------------------------------------------------------------------------------
 // persistent, software-pipelined onesweep pass (8-bit digits)
 //
-// Measured on MI355X (harness/exp/onesweep_exp.hip): the non-persistent pass above
-// spends ~40 % of each tile waiting on the decoupled look-back, because the
-// inclusive-prefix chain advances only as fast as tiles finish their walks under
-// loaded memory latency.  Here each workgroup loops over dynamically acquired tiles
-// and keeps two in flight: tile A (already ranked and reordered, keys in
-// registers in scatter order) waits for its look-back while the workgroup loads,
-// histograms, publishes and ranks tile B.  Per tile:
-//   * the tile's digit histogram is built first (LDS atomics) and its aggregate
-//     published before ranking, so successors see it early;
-//   * the look-back reads a window of OSP_LBW predecessors per round;
-//   * the stable wave rank uses an LDS atomic-XOR match (one 64-bit lane mask per
-//     digit and wave) instead of 8 ballots per key slot.
-// Dynamic tile ids (atomic counter) order the tiles by acquisition, so a tile only
-// ever waits on tiles whose aggregates are published unconditionally right after
-// their histogram: forward progress holds for any grid size or residency.
+// The non-persistent pass above spends ~40 % of each tile waiting on the decoupled
+// look-back (the inclusive-prefix chain advances only as fast as tiles finish their
+// walks under loaded memory latency).  Here each workgroup loops over dynamically
+// acquired tiles and keeps two in flight: tile A (ranked and reordered, keys in
+// registers in scatter order) waits for its look-back while the workgroup ranks tile B,
+// whose keys were loaded one iteration ahead.  Per iteration:
+//   (top)  A's look-back window (LBW predecessors) and tile C's key loads are issued,
+//          and tid 0 issues the next tile's acquisition atomic;
+//   rank   B's keys are ranked per wave by one returning LDS atomic per key;
+//   (2)    A's look-back completes (waves 0-3, one digit per thread); A's INC published;
+//   (2b)   B's tile histogram is summed from the wave counts, its AGG published, scanned;
+//          A's keys are scattered (groups of 4 sorted slots within one digit run as one
+//          16-B store);
+//   (3)    B's per-wave digit offsets; the acquisition resolved;
+//   (4)    B reordered into LDS, read back in scatter order: B becomes A.
+// Dynamic tile ids order the tiles by acquisition, so a tile only ever waits on tiles
+// acquired earlier, whose aggregates are published unconditionally after their rank:
+// forward progress holds for any grid size or residency.  Every spin is bounded.
+// The measured history of this loop (shapes, barriers, prefetch, store widths,
+// acquisition) is in DESIGN.md §3.1; the variants measured slower are gone from here.
 // ---------------------------------------------------------------------------------
-// Phase stamps (diagnostic builds only, -DOSP_STAMPS): each wave sums the shader-clock
-// cycles it spends in each phase of the tile loop and adds them into g_osp_stamps at
-// exit; labsort_exp_stamps reads them.  OSP_T(i, w) closes phase i after waiting for
-// (w & 1) global memory / (w & 2) LDS operations to complete.
-#ifndef OSP_STAMP_W0
-#define OSP_STAMP_W0 1
-#endif
-#ifdef OSP_STAMPS
-__device__ unsigned long long g_osp_stamps[16];
-#define OSP_T(i, w)                                                              \
-    do {                                                                         \
-        if ((w) == 1) __builtin_amdgcn_s_waitcnt(0x0F70);                       \
-        if ((w) == 2) __builtin_amdgcn_s_waitcnt(0xC07F);                       \
-        if ((w) == 3) __builtin_amdgcn_s_waitcnt(0);                            \
-        const unsigned long long t_ = __builtin_amdgcn_s_memtime();              \
-        st_[i] += t_ - tp_;                                                      \
-        tp_ = t_;                                                                \
-    } while (0)
-#define OSP_CNT(x) (x)
-#else
-#define OSP_T(i, w) \
-    do {            \
-    } while (0)
-#define OSP_CNT(x) \
-    do {           \
-    } while (0)
-#endif
-
-// key stream accesses of the onesweep pass (LABSORT_OSP_NT bit 0: nontemporal scatter
-// stores; key loads: LABSORT_NT_LOADS & NT_OSP)
-__device__ __forceinline__ void osp_store(uint32_t *p, uint32_t v) {
-    if constexpr (LABSORT_OSP_NT & 1) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
-__device__ __forceinline__ uint32_t osp_load(const uint32_t *p) { return ld_stream<NT_OSP>(p); }
-
-// LABSORT_OSP_BUF: the pass's key loads and scatter stores go through buffer
-// descriptors (32-bit per-lane offsets instead of 64-bit addresses: fewer VGPRs, so
-// fewer spills whose reloads drain the wave's outstanding stores), and each segment's
-// output bases live in LDS (read once per launch), so A's delta no longer waits on a
-// global load issued behind tile C's prefetched keys.
-#ifndef LABSORT_OSP_BUF
-#define LABSORT_OSP_BUF 1
-#endif
-constexpr bool OSP_BUF = LABSORT_OSP_BUF != 0;
-// LABSORT_OSP_2BAR: two workgroup barriers per tile instead of four.  After barrier (2)
-// every wave reads all waves' digit counts of B (one 16-B LDS read per wave row and lane,
-// 4 digits per lane), scans them itself and writes its own digit offsets, so the
-// aggregate scan's barrier (2b) and the offsets' barrier (3) go; wave 0 publishes B's
-// aggregate.  Keys-only passes with the histogram after the rank (the default variant).
-#ifndef LABSORT_OSP_2BAR
-#define LABSORT_OSP_2BAR 0
-#endif
-constexpr bool OSP_2BAR = LABSORT_OSP_2BAR != 0;
-// LABSORT_OSP_ST4: each lane scatters groups of 4 consecutive sorted slots; a group within
-// one digit run (4 consecutive destinations) is one 16-B store, a group spanning a run
-// edge or the tile's end falls back to 4-B stores.  A quarter of the store instructions
-// carry the bulk of the keys (the pass's issue is paced by the memory queue).
-#ifndef LABSORT_OSP_ST4
-#define LABSORT_OSP_ST4 1  // r26: 0.472 -> 0.464 ms per pass (uniform), 0.474 -> 0.454 (sorted)
-#endif
-// LABSORT_OSP_W0SCAN: wave 0 alone sums B's 16 wave counts (4 digits per lane, 16-B LDS
-// reads), scans them with one wave scan, publishes B's aggregate and writes every wave's
-// digit offsets, while the other waves issue A's scatter: no cross-wave scan, so the
-// aggregate's barrier (2b) goes (three barriers per tile).  Keys-only passes with the
-// histogram after the rank (the default variant).
-// LABSORT_OSP_JCOUNT (timing build): each pass also counts (top nibble of its digit,
-// next active digit) per key in LDS and flushes the 4096 counts with device atomics at
-// exit -- what counting the next pass's segment histograms in the pass would cost
-#ifndef LABSORT_OSP_W0SCAN
-#define LABSORT_OSP_W0SCAN 0
-#endif
-constexpr bool OSP_W0SCAN = LABSORT_OSP_W0SCAN != 0;
-#ifndef LABSORT_OSP_EARLY_ACQ
-#define LABSORT_OSP_EARLY_ACQ 1  // r26: 0.4906 -> 0.4729 ms per pass at 2^28 (barrier 3: 11.9 -> 7.1 % of wave time)
-#endif
-constexpr bool OSP_EARLY_ACQ = LABSORT_OSP_EARLY_ACQ != 0;
-#ifndef LABSORT_OSP_MATCH
-#define LABSORT_OSP_MATCH 1  // the LDS match buffer for the rank's fallback (0: 8-ballot fallback)
-#endif
-#ifndef LABSORT_OSP_LBASE
-#define LABSORT_OSP_LBASE 1  // the segments' output bases in LDS (else read from the SegPlan)
-#endif
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t osp_rsrc(const uint32_t *p, uint32_t n) {
     const uint64_t a = (uint64_t)p;  // wave-uniform: readfirstlane lets the compiler prove it
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
     return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(n * 4u), 0x00020000);
 }
-constexpr int OSP_BUF_NT = (LABSORT_NT_LOADS & NT_OSP) ? 2 : 0;  // aux bit 1 = nt
+constexpr int OSP_BUF_NT = (NT_LOADS & NT_OSP) ? 2 : 0;  // aux bit 1 = nontemporal
 
+// ---- gathered tile loads: the first onesweep pass after the local pass (lsweep.hip) ----
+// Its logical input is the local pass's digit-0 order: run e = (digit d, tile t) of ~64
+// keys at address sr[e], logical start ls[e] (k_lscan's tables).  Per tile the runs that
+// meet it are marked in LDS -- a 64-bit start mask per 64-position block and the
+// blocks' prefix counts -- with each marked run's delta (source - logical position), so a
+// key slot (64 consecutive positions = one block) finds every lane's source address with
+// one broadcast LDS read, a popcount and one delta read, and the 16 loads of a lane issue
+// back to back.  More than GTH_KMAX runs in one tile (rare: many tiny digit-0 runs):
+// each lane searches the tables instead.
+constexpr int GTH_KMAX = 1024;
+struct GthS {
+    uint64_t mask[OSP_TILE / 64];  // run-start bits of each 64-position block of the tile
+    uint32_t pre[OSP_TILE / 64];   // set bits in the blocks before
+    int32_t delta[GTH_KMAX];       // per marked run, in order: source address - logical position
+    uint32_t over, e0, e1, pad;    // over: the slow path (per-lane table search over runs e0..e1)
+};
+struct GthPair {
+    GthS s[2];  // the next tile's structure is built while the current one's is used
+};
+struct GthNone {};
 
+// first run index e0 and last e1 of logical tile range [L0, L0 + nv) (inside the aligned
+// logical tile L0 / OSP_TILE)
+__device__ __forceinline__ void gth_range(const GthTables &tb, uint32_t L0, uint32_t &e0, uint32_t &e1) {
+    const uint32_t k = L0 / (uint32_t)OSP_TILE;
+    e0 = tb.first[k];
+    e1 = tb.first[k + 1];
+}
+// run entry `tid` of runs e0..e1: start a, end b (the next run's start), source s
+__device__ __forceinline__ void gth_run(const GthTables &tb, uint32_t e0, uint32_t e1, uint32_t tid, uint32_t &a,
+                                        uint32_t &b, uint32_t &s) {
+    a = b = s = 0u;
+    if (e1 - e0 < (uint32_t)GTH_KMAX && tid <= e1 - e0) {
+        a = tb.ls[e0 + tid];
+        b = tb.ls[e0 + tid + 1];
+        s = tb.sr[e0 + tid];
+    }
+}
+__device__ __forceinline__ bool gth_meets(uint32_t a, uint32_t b, uint32_t L0, uint32_t nv) {
+    return b > a && b > L0 && a < L0 + nv;
+}
+// (after the clear and a barrier) mark the start of a run that meets the tile
+__device__ __forceinline__ void gth_mark(GthS &S, uint32_t a, uint32_t b, uint32_t L0, uint32_t nv) {
+    if (gth_meets(a, b, L0, nv)) {
+        const uint32_t rel = a > L0 ? a - L0 : 0u;
+        atomicOr(reinterpret_cast<unsigned long long *>(&S.mask[rel >> 6]), 1ull << (rel & 63u));
+    }
+}
+// (one wave, after a barrier) the blocks' prefix counts, 4 blocks per lane
+__device__ __forceinline__ void gth_prefix(GthS &S, uint32_t lane) {
+    static_assert(OSP_TILE / 64 == 4 * WAVE, "4 blocks per lane");
+    uint32_t c[4], sum = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        c[i] = (uint32_t)__popcll(S.mask[4 * lane + i]);
+        sum += c[i];
+    }
+    uint32_t x = sum;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= (uint32_t)off) x += y;
+    }
+    uint32_t e = x - sum;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        S.pre[4 * lane + i] = e;
+        e += c[i];
+    }
+}
+// (after a barrier) the marked run's delta at its rank among the marked runs
+__device__ __forceinline__ void gth_delta(GthS &S, uint32_t a, uint32_t b, uint32_t s, uint32_t L0, uint32_t nv) {
+    if (gth_meets(a, b, L0, nv)) {
+        const uint32_t rel = a > L0 ? a - L0 : 0u, blk = rel >> 6;
+        const uint32_t r = S.pre[blk] + (uint32_t)__popcll(S.mask[blk] & ((1ull << (rel & 63u)) - 1ull));
+        S.delta[r] = (int32_t)(s - a);
+    }
+}
+// keys of logical tile [L0, L0 + nv) in the wave's blocked layout (slot j of wave w = the
+// 64 positions of block w * KPT + j); sentinels past nv
+template <int KPT>
+__device__ __forceinline__ void gth_load(const GthS &S, const GthTables &tb, __amdgpu_buffer_rsrc_t rin, uint32_t L0,
+                                         uint32_t nv, uint32_t wid, uint32_t lane, uint32_t sentinel, int nt,
+                                         uint32_t (&k)[KPT]) {
+    if (!S.over) {
+        uint32_t addr[KPT];
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t blk = wid * KPT + (uint32_t)j, p = blk * 64u + lane;
+            const uint64_t m = S.mask[blk];  // (one address per wave: a broadcast read)
+            const uint32_t r = S.pre[blk] + (uint32_t)__popcll(m & ((2ull << lane) - 1ull)) - 1u;
+            addr[j] = L0 + p + (uint32_t)S.delta[r < (uint32_t)GTH_KMAX ? r : 0u];
+        }
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            // (nontemporal policy bits as the plain loads; past nv the address is garbage
+            // and the key replaced: buffer loads out of range return 0)
+            const uint32_t v = nt ? __builtin_amdgcn_raw_buffer_load_b32(rin, addr[j] * 4u, 0, 2)
+                                  : __builtin_amdgcn_raw_buffer_load_b32(rin, addr[j] * 4u, 0, 0);
+            k[j] = (wid * KPT + (uint32_t)j) * 64u + lane < nv ? v : sentinel;
+        }
+    } else {
+        // many (mostly tiny) runs: each lane searches the run starts for its positions
+#pragma unroll 1
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t p = (wid * KPT + (uint32_t)j) * 64u + lane;
+            uint32_t v = sentinel;
+            if (p < nv) {
+                const uint32_t P = L0 + p;
+                uint32_t lo = S.e0, hi = S.e1 + 1u;  // ls[lo] <= P < ls[hi]
+                while (hi - lo > 1u) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (tb.ls[mid] <= P) lo = mid;
+                    else hi = mid;
+                }
+                v = __builtin_amdgcn_raw_buffer_load_b32(rin, (tb.sr[lo] + (P - tb.ls[lo])) * 4u, 0, 0);
+            }
+            k[j] = v;
+        }
+    }
+}
 
-template <bool MATCH, bool KV = false>
+template <bool KV, bool GATHER = false>
 struct OspSmem {
     static constexpr int BLOCK = KV ? OSP_KV_BLOCK : OSP_BLOCK;  // threads (key/value: its own shape)
     static constexpr int R = 256, W = BLOCK / WAVE, TILE = OSP_TILE;
-    uint32_t keys[TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0)];  // padded: see osp_pad
-    uint32_t vals[KV ? TILE + (LABSORT_OSP_PAD ? TILE / 32 : 0) : 1];  // key/value: payloads, reordered alike
-    uint32_t wh[W * R];
-    uint64_t match[MATCH && !KV && OSP_TILE <= 16384 && LABSORT_OSP_MATCH ? W * R : 1];  // (no room beside bigger tiles)
+    uint32_t keys[TILE + TILE / 32];     // reorder buffer, padded (osp_pad)
+    uint32_t vals[KV ? TILE + TILE / 32 : 1];  // key/value: payloads, reordered alike
+    uint32_t wh[W * R];                  // per-wave digit counters, then offsets
+    uint64_t match[KV ? 1 : W * R];      // rank fallback (LDS match) if the lane-order check fails
     uint32_t probe[WAVE];
     uint32_t ordered;
-    uint32_t hist[R];
-    uint32_t delta[R];
-    uint32_t base[OSP_BUF && !KV && LABSORT_OSP_LBASE ? NSEG * R : 1];  // the segments' output bases (SegPlan::base)
-    uint32_t woff[OSP_2BAR && !KV ? W * R : 1];  // two-barrier loop: each wave's digit offsets
-    uint32_t agg[(OSP_2BAR || OSP_W0SCAN) && !KV ? R : 1];   // two-barrier / wave-0 scan: B's tile
-    uint32_t dst0[(OSP_2BAR || OSP_W0SCAN) && !KV ? R : 1];  //   histogram and digit starts
-    uint32_t jh[LABSORT_OSP_JCOUNT && !KV ? 4096 : 1];       // in-pass joint counts (timing build)
+    uint32_t delta[R];                   // A: output position of its slot 0 per digit
+    uint32_t base[KV ? 1 : NSEG * R];    // the segments' output bases (SegPlan::base)
     uint32_t start[NSEG + 1];
     uint32_t tpre[NSEG + 1];
     uint32_t wsum[8];
-    uint32_t next, next2;
+    uint32_t next, next2, next3;
+    std::conditional_t<GATHER, GthPair, GthNone> g;  // gathered loads: two run structures
 };
 
 constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 
-// RANK: how a wave ranks its keys stably per digit:
-//   OSP_RANK_BALLOT: peers of a digit by 8 ballots (VALU only), counter read + update;
-//   OSP_RANK_MATCH:  peers by an LDS atomic-XOR of lane bits, counter read + update;
-//   OSP_RANK_ATOMIC: one returning LDS atomic add per key on the wave's counter.  The
-//                    rank is stable because gfx950's LDS services the lanes of one
-//                    atomic instruction that hit one address in ascending lane order.
-//                    The ISA does not promise that order, so every workgroup first
-//                    checks it (lds_lane_ordered) and ranks by OSP_RANK_MATCH if the
-//                    check fails.
-// HIST_FIRST: tile histogram by LDS atomics before ranking, aggregate published
-// early (else summed from the per-wave rank counters after ranking).
-// KV: key/value pairs: each payload (vbufs, selected by the plan
-// like the keys) is loaded with its key, reordered in a second LDS buffer and
-// scattered to its key's destination.  The LDS has no room for the match buffer then
-// (the rank falls back to 8 ballots if the lane-order check fails) nor for the bases
-// table, and the registers none for the next tile's prefetch.
-template <int RANK, bool HIST_FIRST, bool KV = false>
-__global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
-                             OSP_BLOCKS_PER_CU *(KV ? OSP_KV_BLOCK : OSP_BLOCK) / 256) void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass,
-                                                          uint32_t n, uint32_t flip, const SegPlan *__restrict__ sp,
-                                                          uint32_t *lookback, uint32_t *counter, uint32_t *err,
-                                                          Bufs vbufs, uint32_t *jout = nullptr) {
-    using S = OspSmem<RANK != OSP_RANK_BALLOT, KV>;
-#ifndef LABSORT_OSP_KV_PF
-#define LABSORT_OSP_KV_PF 0  // r26 A/B at 2^28 pairs: 0.830 ms per pass without, 1.018 with (27 VGPRs spilled)
-#endif
-    // next tile's keys loaded one iteration ahead (key/value: the keys only; B's payloads
-    // are loaded at the top of B's iteration, and first used by B's reorder)
-    constexpr bool PF = OSP_PREFETCH && (!KV || LABSORT_OSP_KV_PF);
-#ifndef LABSORT_OSP_KV_LDSV
-#define LABSORT_OSP_KV_LDSV 0  // r26: 0.843 ms per pass with, 0.830 without
-#endif
-    // key/value: A's payloads are scattered straight from the LDS reorder buffer (they
-    // stay there until B's reorder, after barrier 3), not held in 16 VGPRs
-    constexpr bool LDSV = KV && LABSORT_OSP_KV_LDSV;
-    constexpr bool LBASE = OSP_BUF && !KV && LABSORT_OSP_LBASE;  // bases table in LDS
-    constexpr bool TWO_BAR = OSP_2BAR && !KV && !HIST_FIRST;
-    constexpr bool W0 = OSP_W0SCAN && !TWO_BAR && !KV && !HIST_FIRST;
-    // early acquisition with the prefetch only: the key/value pass (no prefetch) measured
-    // 0.978 vs 0.932 ms per pass with it (profiles/r26_ab_early_acquire.txt)
-#ifndef LABSORT_OSP_KV_EACQ
-#define LABSORT_OSP_KV_EACQ 0
-#endif
-    constexpr bool EACQ = OSP_EARLY_ACQ && (PF || (KV && LABSORT_OSP_KV_EACQ));
-    static_assert(!KV || OSP_BUF, "key/value passes use the buffer-descriptor loads and stores");
-    constexpr int R = S::R, W = S::W, TILE = S::TILE, BLK = S::BLOCK, KPT = TILE / BLK, LBW = OSP_LBW, LBW2 = OSP_LBW2;
-    static_assert(BLK >= 512 && R <= BLK && NSEG == 16 && KPT * BLK == TILE, "digit threads = waves 0-3; c & 15 = segment");
-    // (key/value: 0.865-0.900 vs 0.843-0.853 ms per pass with it, profiles/r26_ab_st4.txt)
-#ifndef LABSORT_OSP_KV_ST4
-#define LABSORT_OSP_KV_ST4 0  // key/value: 1 = keys and payloads grouped (slower, r26), 2 = keys only
-#endif
-    constexpr bool ST4 = LABSORT_OSP_ST4 && OSP_BUF && (!KV || LABSORT_OSP_KV_ST4) && !LDSV && !OSP_LDS_SCATTER &&
-                         KPT % 4 == 0;
-    constexpr bool ST4V = KV && LABSORT_OSP_KV_ST4 == 1;  // payloads as 16-B groups too
-#ifndef LABSORT_OSP_LD4
-#define LABSORT_OSP_LD4 0
-#endif
-    // LD4: 16-B key loads in the first active pass of keys-only sorts (see load_tile)
-    constexpr bool LD4 = LABSORT_OSP_LD4 && OSP_BUF && !KV && KPT % 4 == 0;
-    const bool ld4_pass = LD4 && plan->prev[pass] == NEXT_NONE;
+// KV: key/value pairs: each payload (vbufs, selected by the plan like
+// the keys) is loaded with its key, reordered in a second LDS buffer and scattered to
+// its key's destination.  No room in LDS for the match buffer (the rank's fallback is
+// then 8 ballots) nor the bases table, and no registers for the next tile's prefetch:
+// 512-thread workgroups, the acquisition at the end of the iteration.
+// GATHER: the first launch after the local pass (lsweep.hip): tile C's keys are gathered
+// through the run tables tb (gth_load); tile D's run structure is built during the
+// iteration before (its table entries loaded at the top, marked after barrier 2, its
+// prefix counts after 2b by the last wave, its deltas after 3), so three tiles are
+// acquired ahead (B, C, D) instead of two.
+template <bool KV = false, bool GATHER = false>
+__global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK, (KV ? OSP_KV_BLOCK : OSP_BLOCK) / 256)
+void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n, uint32_t flip,
+                  const SegPlan *__restrict__ sp, uint32_t *lookback, uint32_t *counter, uint32_t *err, Bufs vbufs,
+                  GthTables tb) {
+    static_assert(!(KV && GATHER), "key/value sorts take the histogram path");
+    using S = OspSmem<KV, GATHER>;
+    constexpr bool PF = !KV;  // next tile's keys loaded one iteration ahead
+    constexpr bool ST4 = !KV;  // grouped 16-B scatter stores (r26; the key/value pass measured 2-5 % slower with them)
+    constexpr int R = S::R, W = S::W, TILE = S::TILE, BLK = S::BLOCK, KPT = TILE / BLK, LBW = OSP_LBW;
+    static_assert(BLK >= 512 && NSEG == 16 && KPT * BLK == TILE && KPT % 4 == 0, "digit threads = waves 0-3");
     __shared__ S sm;
 
     const uint32_t srcsel = plan->src[pass];
@@ -873,8 +921,6 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
             // pass 0's launch copies it (api.hip launches no final copy for in != out)
             const uint4 *src = reinterpret_cast<const uint4 *>(bufs.p[SEL_IN]);
             uint4 *dst = reinterpret_cast<uint4 *>(bufs.p[SEL_OUT]);
-            const uint32_t *vsrc = KV ? vbufs.p[SEL_IN] : nullptr;
-            uint32_t *vdst = KV ? vbufs.p[SEL_OUT] : nullptr;
             const size_t stride = (size_t)gridDim.x * BLK, g0 = (size_t)blockIdx.x * BLK + threadIdx.x;
             if (((((uintptr_t)src) | ((uintptr_t)dst)) & 15u) == 0) {
                 for (size_t i = g0; i < n / 4; i += stride) dst[i] = src[i];
@@ -883,32 +929,28 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                 for (size_t i = g0; i < n; i += stride) bufs.p[SEL_OUT][i] = bufs.p[SEL_IN][i];
             }
             if constexpr (KV)
-                for (size_t i = g0; i < n; i += stride) vdst[i] = vsrc[i];
+                for (size_t i = g0; i < n; i += stride) vbufs.p[SEL_OUT][i] = vbufs.p[SEL_IN][i];
         }
         return;
     }
-    const uint32_t *__restrict__ in = bufs.p[srcsel];
-    uint32_t *__restrict__ out = bufs.p[plan->dst[pass]];
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t shift = (uint32_t)pass * 8u;
+    const uint32_t shift = plan->digit[pass] * 8u;
     const uint32_t sentinel = ~flip;  // digit 255 in every pass: ranks after all real keys
-    // tile id = l * NSEG + segment (tile l of the segment)
+    // tile id c = l * NSEG + segment (tile l of the segment)
     constexpr uint32_t segbits = 4, segmask = NSEG - 1;
-    // counter groups: G groups of NSEG / G segments, group g = segments {g, g + G, ...};
-    // one group when there is a single chain (mode 2)
-    const bool grouped = OSP_XCD && sp->mode != 2u;
+    // XCD-grouped acquisition: counter group g = segments {g, g + 8}; a workgroup takes
+    // the tiles of its own XCD's group first, then helps the others (consecutive tiles
+    // of a chain then meet in one L2).  One group when there is a single chain (mode 2).
+    const bool grouped = sp->mode != 2u;
     const uint32_t gbits = grouped ? 3u : 0u, G = 1u << gbits;
     const uint32_t lbits = sp->segbits - gbits, lmask = (1u << lbits) - 1u;
     const uint32_t climit = sp->maxt << lbits;
 
     for (uint32_t i = tid; i < (uint32_t)(W * R); i += BLK) sm.wh[i] = 0u;
-    constexpr bool JC = LABSORT_OSP_JCOUNT && !KV;
-    const uint32_t jnext = JC && jout ? plan->next[pass] : NEXT_NONE;
-    const uint32_t jshift = 8u * (jnext & 3u);
-    if constexpr (JC)
-        for (uint32_t i = tid; i < 4096u; i += BLK) sm.jh[i] = 0u;
-    if constexpr (LBASE)
+    if constexpr (!KV)
         for (uint32_t i = tid; i < (uint32_t)(NSEG * R); i += BLK) sm.base[i] = sp->base[i];
+    const uint32_t *__restrict__ in = bufs.p[srcsel];
+    uint32_t *__restrict__ out = bufs.p[plan->dst[pass]];
     const __amdgpu_buffer_rsrc_t rin = osp_rsrc(in, n), rout = osp_rsrc(out, n);
     const __amdgpu_buffer_rsrc_t rvin = osp_rsrc(KV ? vbufs.p[srcsel] : in, n),
                                  rvout = osp_rsrc(KV ? vbufs.p[plan->dst[pass]] : out, n);
@@ -916,11 +958,8 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
         sm.start[tid] = sp->start[tid];
         sm.tpre[tid] = sp->tpre[tid];
     }
-    if (tid < (uint32_t)R) sm.hist[tid] = 0u;
-    // tile acquisition: c -> segment c & 15, tile c >> 4 of that segment; ids past a
-    // segment's last tile are skipped, so every segment's tiles are acquired in order
-    // (tid 0 only) own group first, then the others in turn; a group's counter hands out
-    // its segments' tiles in order, whoever takes them
+    // tile acquisition (tid 0): c -> segment c & 15, tile c >> 4 of that segment; ids past
+    // a segment's last tile are skipped, so every segment's tiles are acquired in order
     const uint32_t home = grouped ? (__builtin_amdgcn_s_getreg((3 << 11) | 20) & (G - 1u)) : 0u;  // HW_REG_XCC_ID
     uint32_t gk = 0;
     auto acquire = [&]() {
@@ -936,11 +975,10 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
         }
         return OSP_DONE;
     };
-    // LABSORT_OSP_EARLY_ACQ: the in-loop acquisition's counter increment is issued by tid 0
-    // at the top of the iteration and its result consumed before barrier (3), so the
-    // atomic's round trip overlaps the iteration instead of holding every wave at the
-    // barrier; the segment's tile count comes from LDS
-    auto acquire_done = [&](uint32_t c) {  // c: atomicAdd(counter + group gk), issued earlier
+    // early acquisition: the counter increment was issued by tid 0 at the top of the
+    // iteration and is resolved here, before barrier (3), so its round trip overlaps the
+    // iteration instead of holding every wave at the barrier (r26: 0.491 -> 0.473 ms/pass)
+    auto acquire_done = [&](uint32_t c) {
         while (gk < G) {
             const uint32_t grp = (home + gk) & (G - 1u);
             if (c >= climit) {
@@ -957,33 +995,27 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
         const uint32_t c0 = acquire();
         sm.next = c0;
         sm.next2 = (PF && c0 != OSP_DONE) ? acquire() : OSP_DONE;
+        sm.next3 = (GATHER && sm.next2 != OSP_DONE) ? acquire() : OSP_DONE;
     }
-    if (RANK == OSP_RANK_ATOMIC && wid == 0) {
+    if (wid == 0) {
         const bool ord = lds_lane_ordered(sm.probe, lane);
         if (lane == 0) sm.ordered = ord ? 1u : 0u;
     }
     __syncthreads();
-    // OSP_PREFETCH: tile B's keys were loaded one iteration ahead (while the previous
-    // B was ranked and A scattered); the loads of the tile after B (C) are issued at
-    // the top of B's iteration into kN.
-    uint32_t cB = sm.next, cC = sm.next2;
-    const bool atomic_rank = RANK == OSP_RANK_ATOMIC && __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
+    uint32_t cB = sm.next, cC = sm.next2, cD = sm.next3;
+    const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
 
     // carried state of tile A (slot = look-back slot, lo = slot of its segment's first tile)
     uint32_t slotA = OSP_DONE, loA = 0, segA = 0, nvalidA = 0;
     uint32_t kA[KPT];
-    uint32_t vA[KV ? KPT : 1];  // key/value: A's payloads in scatter order (unless LDSV)
+    uint32_t vA[KV ? KPT : 1];
     uint32_t lwA[LBW];
     uint32_t aggA = 0, dstartA = 0;
     uint32_t *wh = sm.wh + wid * R;
-    uint64_t *wm = sm.match + wid * R;
-#ifdef OSP_STAMPS
-    unsigned long long st_[10] = {}, tp_ = __builtin_amdgcn_s_memtime();
-    unsigned long long lbr_ = 0, lbs_ = 0, lbw_ = 0, lbt_ = 0;  // look-back rounds, stalls, tiles walked, look-backs
-#endif
-    // input range of tile c: [beg, beg + nvalid)
-    // Tiles are aligned to TILE-key boundaries of the input (coalesced, line-aligned
-    // wave loads): a segment's first tile runs from its start to the next boundary.
+    uint64_t *wm = sm.match + (KV ? 0 : wid * R);
+    // input range of tile c: [beg, beg + nvalid).  Tiles are aligned to TILE-key
+    // boundaries of the input (line-aligned wave loads): a segment's first tile runs
+    // from its start to the next boundary.
     auto tile_range = [&](uint32_t c, uint32_t &beg, uint32_t &nvalid) {
         const uint32_t sg = c & segmask, l = c >> segbits;
         const uint32_t s0 = sm.start[sg], a0 = s0 - s0 % (uint32_t)TILE;
@@ -991,60 +1023,21 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
         const uint32_t tend = a0 + (l + 1u) * (uint32_t)TILE, send = sm.start[sg + 1];
         nvalid = (tend < send ? tend : send) - beg;
     };
-    // keys of tile c in the wave's blocked layout; sentinels (digit 255) past its end
+    // keys of tile c in the wave's blocked layout (buffer loads: out-of-range offsets read
+    // 0, replaced by the sentinel, digit 255)
     auto load_tile = [&](uint32_t c, uint32_t (&k)[KPT]) {
         uint32_t beg, nv;
         tile_range(c, beg, nv);
         const uint32_t woff = wid * (KPT * WAVE) + lane;
-        const uint32_t *src = in + beg + woff;
-        if constexpr (OSP_BUF) {  // out-of-range offsets read 0 (replaced by the sentinel)
-            const uint32_t o = (beg + woff) * 4u;
-            if (LD4 && ld4_pass && nv == (uint32_t)TILE) {
-                // first active pass of a keys-only sort: the order of equal digits within a
-                // tile is free (nothing earlier to keep), so each lane loads 4 consecutive keys
-                // per 256-key chunk with one 16-B load and ranks them as its slots
-                const uint32_t o4 = (beg + wid * (KPT * WAVE) + 4u * lane) * 4u;
-#pragma unroll
-                for (int q = 0; q < KPT / 4; ++q) {
-                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rin, o4 + q * 4 * WAVE * 4, 0, OSP_BUF_NT);
-                    k[4 * q] = v.x;
-                    k[4 * q + 1] = v.y;
-                    k[4 * q + 2] = v.z;
-                    k[4 * q + 3] = v.w;
-                }
-            } else if (nv == (uint32_t)TILE) {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) k[j] = __builtin_amdgcn_raw_buffer_load_b32(rin, o + j * WAVE * 4, 0, OSP_BUF_NT);
-            } else {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rin, o + j * WAVE * 4, 0, OSP_BUF_NT);
-                    k[j] = woff + j * WAVE < nv ? v : sentinel;
-                }
-            }
-            return;
-        }
+        const uint32_t o = (beg + woff) * 4u;
         if (nv == (uint32_t)TILE) {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) k[j] = osp_load(src + j * WAVE);
+            for (int j = 0; j < KPT; ++j) k[j] = __builtin_amdgcn_raw_buffer_load_b32(rin, o + j * WAVE * 4, 0, OSP_BUF_NT);
         } else {
-            // past the tile's end: load its last key instead and substitute the sentinel.
-            // The load is kept unconditional (the empty asm uses its value): a
-            // conditional load is speculated by the compiler into a FLAT load of a
-            // select between the key's address and a stack slot holding the sentinel.
-            // FLAT loads complete out of order, so every later use of any load result
-            // then waited vmcnt(0) lgkmcnt(0) -- the look-back window was waited for at
-            // the top of the iteration instead of behind B's rank.
-            uint32_t v[KPT];
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
-                const uint32_t i = woff + j * WAVE;
-                v[j] = osp_load(in + beg + (i < nv ? i : nv - 1u));
-            }
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                asm volatile("" : "+v"(v[j]));
-                k[j] = woff + j * WAVE < nv ? v[j] : sentinel;
+                const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rin, o + j * WAVE * 4, 0, OSP_BUF_NT);
+                k[j] = woff + j * WAVE < nv ? v : sentinel;
             }
         }
     };
@@ -1058,8 +1051,47 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
     };
     uint32_t kB[KPT], kN[PF ? KPT : 1];
     uint32_t vB[KV ? KPT : 1];
-    if constexpr (PF)
+    uint32_t sc = 0;            // GATHER: the structure of tile C (D's is built in the other)
+    uint32_t e0D = 0, e1D = 0;  // GATHER: the run range of tile D
+    if constexpr (GATHER) {
+        // B's and C's run structures (once per workgroup, not pipelined), B's keys
+        auto build = [&](uint32_t c, GthS &G) {  // block-uniform
+            uint32_t L0 = 0, nv = 0, e0 = 0, e1 = 0, a = 0, b = 0, s = 0;
+            if (c != OSP_DONE) {
+                tile_range(c, L0, nv);
+                gth_range(tb, L0, e0, e1);
+                gth_run(tb, e0, e1, tid, a, b, s);
+            }
+            if (tid < (uint32_t)(OSP_TILE / 64)) G.mask[tid] = 0ull;
+            if (tid == 0) {
+                G.over = c != OSP_DONE && e1 - e0 >= (uint32_t)GTH_KMAX;
+                G.e0 = e0;
+                G.e1 = e1;
+            }
+            __syncthreads();
+            gth_mark(G, a, b, L0, nv);
+            __syncthreads();
+            if (wid == 0) gth_prefix(G, lane);
+            __syncthreads();
+            gth_delta(G, a, b, s, L0, nv);
+            __syncthreads();
+        };
+        build(cB, sm.g.s[0]);
+        if (cB != OSP_DONE) {
+            uint32_t beg, nv;
+            tile_range(cB, beg, nv);
+            gth_load<KPT>(sm.g.s[0], tb, rin, beg, nv, wid, lane, sentinel, OSP_BUF_NT, kN);
+        }
+        build(cC, sm.g.s[1]);
+        sc = 1;
+        if (cD != OSP_DONE) {
+            uint32_t beg, nv;
+            tile_range(cD, beg, nv);
+            gth_range(tb, beg, e0D, e1D);
+        }
+    } else if constexpr (PF) {
         if (cB != OSP_DONE) load_tile(cB, kN);
+    }
 
     for (;;) {
         if constexpr (PF) {  // B's keys, loaded one iteration ahead
@@ -1067,65 +1099,58 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
             for (int j = 0; j < KPT; ++j) kB[j] = kN[j < (PF ? KPT : 1) ? j : 0];
         }
         const bool haveB = cB != OSP_DONE;
-        uint32_t acq_c = 0;  // tid 0: the early counter increment (EARLY_ACQ)
-        if (EACQ && tid == 0 && (!PF || cC != OSP_DONE) && gk < G)
-            acq_c = atomicAdd(counter + ((home + gk) & (G - 1u)), 1u);
+        uint32_t acq_c = 0;  // tid 0: the early counter increment
+        const uint32_t cLast = GATHER ? cD : cC;  // the last tile acquired so far
+        if (PF && tid == 0 && cLast != OSP_DONE && gk < G) acq_c = atomicAdd(counter + ((home + gk) & (G - 1u)), 1u);
         const uint32_t segB = cB & segmask, lB = cB >> segbits;
         const uint32_t loB = haveB ? sm.tpre[segB] : 0u, slotB = loB + lB;
         uint32_t begB = 0, nvalidB = 0;
         if (haveB) tile_range(cB, begB, nvalidB);
         uint32_t rB[KPT / 2];  // wave-local ranks of B, two 16-bit ranks per register
         uint32_t hB = 0, xB = 0;
-        // look-back window of A (its latency hides behind B's load, histogram and rank)
+        // look-back window of A (its latency hides behind B's rank)
         if (slotA != OSP_DONE && tid < (uint32_t)R) {
             const int32_t hi = (int32_t)slotA - 1;
 #pragma unroll
             for (int i = 0; i < LBW; ++i)
                 lwA[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
         }
-        if constexpr (PF) {
+        if constexpr (GATHER) {
+            if (cC != OSP_DONE) {
+                uint32_t begC, nvC;
+                tile_range(cC, begC, nvC);
+                gth_load<KPT>(sm.g.s[sc], tb, rin, begC, nvC, wid, lane, sentinel, OSP_BUF_NT, kN);
+            }
+        } else if constexpr (PF) {
             if (cC != OSP_DONE) load_tile(cC, kN);
-            if constexpr (KV)
-                if (haveB) load_vals(cB, vB);
         } else if (haveB) {
             load_tile(cB, kB);
             if constexpr (KV) load_vals(cB, vB);
         }
-        if (HIST_FIRST && haveB) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j)
-                if ((uint32_t)j * WAVE + wid * (KPT * WAVE) + lane < nvalidB)
-                    atomicAdd(&sm.hist[((kB[j] ^ flip) >> shift) & 255u], 1u);
-        }
-        OSP_T(0, OSP_STAMP_W0);  // look-back issue + B's keys landed (OSP_STAMP_W0 = 0: issue only)
-        if constexpr (HIST_FIRST) __syncthreads();  // (1) histogram of B complete
-        if (haveB) {
-            if (HIST_FIRST && tid < (uint32_t)R) {
-                hB = sm.hist[tid];
-                st_agent(lookback + (size_t)slotB * R + tid, (lB == 0 ? LB_INC : LB_AGG) | hB);
-                xB = hB;
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const uint32_t t = __shfl_up(xB, off);
-                    if (lane >= (uint32_t)off) xB += t;
-                }
-                if (lane == 63) sm.wsum[wid] = xB;
+        // GATHER: tile D's run structure, step 1: clear, table entries
+        uint32_t La = 0, Lb = 0, Ls = 0, L0D = 0, nvD = 0;
+        if constexpr (GATHER) {
+            GthS &GD = sm.g.s[sc ^ 1u];
+            if (tid < (uint32_t)(OSP_TILE / 64)) GD.mask[tid] = 0ull;
+            if (tid == 0) {
+                GD.over = cD != OSP_DONE && e1D - e0D >= (uint32_t)GTH_KMAX;
+                GD.e0 = e0D;
+                GD.e1 = e1D;
             }
-            // stable wave rank of B
+            if (cD != OSP_DONE) {
+                tile_range(cD, L0D, nvD);
+                gth_run(tb, e0D, e1D, tid, La, Lb, Ls);
+            }
+        }
+        if (haveB) {  // stable wave rank of B
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
-                if (JC && jnext != NEXT_NONE) {  // (sentinels count into a bin no segment plan reads: nibble 15, digit 255)
-                    const uint32_t x = kB[j] ^ flip;
-                    __hip_atomic_fetch_add(&sm.jh[((d & 0xF0u) << 4) | ((x >> jshift) & 255u)], 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
                 if (atomic_rank) {
                     const uint32_t r = wave_atomic_rank(wh, d, lane);
                     rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
                 } else {
-                    const uint64_t m = (RANK != OSP_RANK_BALLOT && !KV && OSP_TILE <= 16384 && LABSORT_OSP_MATCH) ? lds_peers(wm + d, lane)
-                                                                                          : match8(d);
+                    const uint64_t m = KV ? match8(d) : lds_peers(wm + d, lane);
                     const uint32_t pre = mbcnt64(m);
                     const uint32_t old = wh[d];
                     if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
@@ -1133,11 +1158,10 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                 }
             }
         }
-        OSP_T(1, 2);  // rank of B
         // complete the look-back of A; publish its inclusive prefix (within its segment)
         if (slotA != OSP_DONE && tid < (uint32_t)R) {
-            // first round: the LBW words loaded at the top of the iteration; later
-            // rounds (each a dependent memory round trip) read LBW2 words at once
+            // first round: the LBW words loaded at the top of the iteration; later rounds
+            // (each a dependent memory round trip) read LBW words at once
             uint32_t excl = 0, spins = 0;
             int32_t hi = (int32_t)slotA - 1;
             int consumed = 0;
@@ -1153,26 +1177,23 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                     }
                 }
             }
-            OSP_CNT(lbw_ += consumed);
             while (!done) {
-                OSP_CNT(++lbr_);
                 hi -= consumed;
                 if (stall) {
-                    OSP_CNT(++lbs_);
                     if (++spins > SPIN_LIMIT) {
                         atomicOr(err, 1u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
                 }
-                uint32_t lw[LBW2];
+                uint32_t lw[LBW];
 #pragma unroll
-                for (int i = 0; i < LBW2; ++i)
+                for (int i = 0; i < LBW; ++i)
                     lw[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
                 consumed = 0;
                 stall = false;
 #pragma unroll
-                for (int i = 0; i < LBW2; ++i) {
+                for (int i = 0; i < LBW; ++i) {
                     if (!done && !stall) {
                         if ((lw[i] & ~LB_VAL) == 0u) stall = true;
                         else {
@@ -1182,184 +1203,67 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                         }
                     }
                 }
-                OSP_CNT(lbw_ += consumed);
             }
-            OSP_CNT(++lbt_);
             if (slotA > loA) st_agent(lookback + (size_t)slotA * R + tid, LB_INC | (excl + aggA));
-            sm.delta[tid] = (LBASE ? sm.base[segA * R + tid] : sp->base[segA * R + tid]) + excl - dstartA;
+            sm.delta[tid] = (KV ? sp->base[segA * R + tid] : sm.base[segA * R + tid]) + excl - dstartA;
         }
-        OSP_T(2, 3);  // look-back completion of A (waves 0-3)
-        __syncthreads();  // (2) delta of A, wave counts and wsum of B
-        OSP_T(3, 0);
-        // two-barrier loop: wave 0 scans B first (it publishes B's aggregate), the other
-        // waves after issuing A's scatter (the stores are the pass's bound: issue them first)
-        auto b_offsets = [&]() {
-            // every wave: B's histogram for digits 4 lane .. 4 lane + 3 and the counts of the
-            // waves before it, from all waves' counters; its own digit offsets from a wave scan
-            uint32_t t4[4] = {0u, 0u, 0u, 0u}, p4[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint4 c = *reinterpret_cast<const uint4 *>(sm.wh + w * R + 4u * lane);
-                t4[0] += c.x;
-                t4[1] += c.y;
-                t4[2] += c.z;
-                t4[3] += c.w;
-                if ((uint32_t)w < wid) {
-                    p4[0] += c.x;
-                    p4[1] += c.y;
-                    p4[2] += c.z;
-                    p4[3] += c.w;
-                }
-            }
-            if (lane == 63u) t4[3] -= (uint32_t)TILE - nvalidB;  // digit 255: the sentinels (last in the tile)
-            const uint32_t s4 = t4[0] + t4[1] + t4[2] + t4[3];
-            uint32_t x = s4;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(x, off);
-                if (lane >= (uint32_t)off) x += y;
-            }
-            uint32_t d4[4];
-            d4[0] = x - s4;
-            d4[1] = d4[0] + t4[0];
-            d4[2] = d4[1] + t4[1];
-            d4[3] = d4[2] + t4[2];
-            *reinterpret_cast<uint4 *>(sm.woff + wid * R + 4u * lane) =
-                uint4{d4[0] + p4[0], d4[1] + p4[1], d4[2] + p4[2], d4[3] + p4[3]};
-            if (wid == 0) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    st_agent(lookback + (size_t)slotB * R + 4u * lane + q, (lB == 0 ? LB_INC : LB_AGG) | t4[q]);
-                *reinterpret_cast<uint4 *>(sm.agg + 4u * lane) = uint4{t4[0], t4[1], t4[2], t4[3]};
-                *reinterpret_cast<uint4 *>(sm.dst0 + 4u * lane) = uint4{d4[0], d4[1], d4[2], d4[3]};
-            }
-        };
-        if (TWO_BAR && haveB && wid == 0) b_offsets();
-        if (W0 && haveB && wid == 0) {
-            // wave 0: B's histogram (4 digits per lane), digit starts, aggregate, and every
-            // wave's digit offsets written over its counts
-            uint32_t t4[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const uint4 c = *reinterpret_cast<const uint4 *>(sm.wh + w * R + 4u * lane);
-                t4[0] += c.x;
-                t4[1] += c.y;
-                t4[2] += c.z;
-                t4[3] += c.w;
-            }
-            const uint32_t sent = lane == 63u ? (uint32_t)TILE - nvalidB : 0u;  // digit 255: the sentinels
-            const uint32_t s4 = t4[0] + t4[1] + t4[2] + t4[3] - sent;
-            uint32_t x = s4;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(x, off);
-                if (lane >= (uint32_t)off) x += y;
-            }
-            uint32_t d4[4];
-            d4[0] = x - s4;
-            d4[1] = d4[0] + t4[0];
-            d4[2] = d4[1] + t4[1];
-            d4[3] = d4[2] + t4[2];
-            t4[3] -= sent;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                st_agent(lookback + (size_t)slotB * R + 4u * lane + q, (lB == 0 ? LB_INC : LB_AGG) | t4[q]);
-            *reinterpret_cast<uint4 *>(sm.agg + 4u * lane) = uint4{t4[0], t4[1], t4[2], t4[3]};
-            *reinterpret_cast<uint4 *>(sm.dst0 + 4u * lane) = uint4{d4[0], d4[1], d4[2], d4[3]};
-            uint4 r = uint4{d4[0], d4[1], d4[2], d4[3]};
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                uint4 *p = reinterpret_cast<uint4 *>(sm.wh + w * R + 4u * lane);
-                const uint4 c = *p;
-                *p = r;
-                r.x += c.x;
-                r.y += c.y;
-                r.z += c.z;
-                r.w += c.w;
-            }
-        }
-        if (!W0 && !TWO_BAR && !HIST_FIRST && haveB) {
+        __syncthreads();  // (2) delta of A, wave counts of B
+        if constexpr (GATHER) gth_mark(sm.g.s[sc ^ 1u], La, Lb, L0D, nvD);  // D, step 2
+        if (haveB && tid < (uint32_t)R) {
             // tile histogram = sum of the per-wave counts; publish B's aggregate, scan it
-            if (tid < (uint32_t)R) {
-                uint32_t tot = 0;
+            uint32_t tot = 0;
 #pragma unroll
-                for (int w = 0; w < W; ++w) tot += sm.wh[w * R + tid];
-                if (tid == (uint32_t)R - 1) tot -= (uint32_t)TILE - nvalidB;  // sentinels
-                hB = tot;
-                st_agent(lookback + (size_t)slotB * R + tid, (lB == 0 ? LB_INC : LB_AGG) | hB);
-                xB = hB;
+            for (int w = 0; w < W; ++w) tot += sm.wh[w * R + tid];
+            if (tid == (uint32_t)R - 1) tot -= (uint32_t)TILE - nvalidB;  // sentinels
+            hB = tot;
+            st_agent(lookback + (size_t)slotB * R + tid, (lB == 0 ? LB_INC : LB_AGG) | hB);
+            xB = hB;
 #pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const uint32_t t = __shfl_up(xB, off);
-                    if (lane >= (uint32_t)off) xB += t;
-                }
-                if (lane == 63) sm.wsum[wid] = xB;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t t = __shfl_up(xB, off);
+                if (lane >= (uint32_t)off) xB += t;
             }
+            if (lane == 63) sm.wsum[wid] = xB;
         }
         if (slotA != OSP_DONE) {
-            if (ST4) {
+            if constexpr (ST4) {
+                // lane holds sorted slots 4 (g BLK + tid) + q: 4 keys in one digit run (their
+                // first and last digits agree) leave as one 16-B store, else 4 dword stores;
+                // a partial tile's sentinels (slot >= nvalidA) go past the array's end: dropped
 #pragma unroll
                 for (int g = 0; g < KPT / 4; ++g) {
-                    const uint32_t i0 = 4u * ((uint32_t)g * BLK + tid);  // slots i0 .. i0 + 3
+                    const uint32_t i0 = 4u * ((uint32_t)g * BLK + tid);
                     uint32_t d[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) d[q] = ((kA[4 * g + q] ^ flip) >> shift) & 255u;
-                    const bool whole = d[0] == d[3] && i0 + 3u < nvalidA;  // sorted: d0 == d3 => all equal
                     const uint32_t dst0 = sm.delta[d[0]] + i0;
-                    if (whole) {
+                    if (d[0] == d[3] && i0 + 3u < nvalidA) {
                         const u32x4 v = {kA[4 * g], kA[4 * g + 1], kA[4 * g + 2], kA[4 * g + 3]};
                         __builtin_amdgcn_raw_buffer_store_b128(v, rout, dst0 * 4u, 0, 0);
-                        if constexpr (ST4V) {
-                            const u32x4 w = {vA[4 * g], vA[4 * g + 1], vA[4 * g + 2], vA[4 * g + 3]};
-                            __builtin_amdgcn_raw_buffer_store_b128(w, rvout, dst0 * 4u, 0, 0);
-                        } else if constexpr (KV) {
-#pragma unroll
-                            for (int q = 0; q < 4; ++q)
-                                __builtin_amdgcn_raw_buffer_store_b32(vA[4 * g + q], rvout, (dst0 + q) * 4u, 0, 0);
-                        }
                     } else {
 #pragma unroll
                         for (int q = 0; q < 4; ++q) {
                             const uint32_t i = i0 + (uint32_t)q;
                             const uint32_t dst = i < nvalidA ? sm.delta[d[q]] + i : n;
                             __builtin_amdgcn_raw_buffer_store_b32(kA[4 * g + q], rout, dst * 4u, 0, 0);
-                            if constexpr (KV) __builtin_amdgcn_raw_buffer_store_b32(vA[4 * g + q], rvout, dst * 4u, 0, 0);
                         }
                     }
-                }
-            } else if (OSP_BUF) {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = (uint32_t)j * BLK + tid;
-                    const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
-                    // a partial tile's sentinels (i >= nvalidA) go past the array's end: dropped
-                    const uint32_t dst = i < nvalidA ? sm.delta[((key ^ flip) >> shift) & 255u] + i : n;
-                    __builtin_amdgcn_raw_buffer_store_b32(key, rout, dst * 4u, 0, (LABSORT_OSP_NT & 1) ? 2 : 0);
-                    if constexpr (KV)
-                        __builtin_amdgcn_raw_buffer_store_b32(LDSV ? sm.vals[osp_pad(i)] : vA[j], rvout, dst * 4u, 0, 0);
-                }
-            } else if (nvalidA == (uint32_t)TILE) {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) {
-                    const uint32_t i = (uint32_t)j * BLK + tid;
-                    const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
-                    osp_store(out + sm.delta[((key ^ flip) >> shift) & 255u] + i, key);
                 }
             } else {
 #pragma unroll
                 for (int j = 0; j < KPT; ++j) {
                     const uint32_t i = (uint32_t)j * BLK + tid;
-                    const uint32_t key = OSP_LDS_SCATTER ? sm.keys[osp_pad(i)] : kA[j];
-                    if (i < nvalidA) osp_store(out + sm.delta[((key ^ flip) >> shift) & 255u] + i, key);
+                    const uint32_t dst = i < nvalidA ? sm.delta[((kA[j] ^ flip) >> shift) & 255u] + i : n;
+                    __builtin_amdgcn_raw_buffer_store_b32(kA[j], rout, dst * 4u, 0, 0);
+                    if constexpr (KV) __builtin_amdgcn_raw_buffer_store_b32(vA[j], rvout, dst * 4u, 0, 0);
                 }
             }
         }
-        if (TWO_BAR && haveB && wid != 0) b_offsets();
-        OSP_T(4, 0);  // aggregate of B, scatter of A issued
         if (!haveB) break;
-        if constexpr (!HIST_FIRST && !TWO_BAR && !W0) __syncthreads();  // (2b) wsum of B
-        OSP_T(5, 0);
-        if (!TWO_BAR && !W0 && tid < (uint32_t)R) {
+        __syncthreads();  // (2b) wave sums of B's digit scan
+        if constexpr (GATHER)
+            if (wid == (uint32_t)W - 1u) gth_prefix(sm.g.s[sc ^ 1u], lane);  // D, step 3
+        if (tid < (uint32_t)R) {
             uint32_t add = 0;
 #pragma unroll
             for (int w = 0; w < 4; ++w)
@@ -1372,87 +1276,60 @@ __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK,
                 sm.wh[w * R + tid] = run;
                 run += c;
             }
-            sm.hist[tid] = 0u;
             dstartA = ds;
         }
-        if (tid == 0)
-            sm.next = (!PF || cC != OSP_DONE) ? (EACQ ? acquire_done(acq_c) : acquire()) : OSP_DONE;
-        OSP_T(6, 0);  // wave offsets (waves 0-3), acquisition
-        if constexpr (!TWO_BAR) __syncthreads();  // (3) wave offsets of B
-        OSP_T(7, 0);
-        const uint32_t *wo = TWO_BAR ? sm.woff + wid * R : wh;
+        if (tid == 0) sm.next = !PF ? acquire() : cLast != OSP_DONE ? acquire_done(acq_c) : OSP_DONE;
+        __syncthreads();  // (3) wave offsets of B
+        uint32_t e0N = 0, e1N = 0;
+        if constexpr (GATHER) {
+            gth_delta(sm.g.s[sc ^ 1u], La, Lb, Ls, L0D, nvD);  // D, step 4
+            const uint32_t cN = sm.next;  // the tile after D: its run range (used next iteration)
+            if (cN != OSP_DONE) {
+                uint32_t beg, nv;
+                tile_range(cN, beg, nv);
+                gth_range(tb, beg, e0N, e1N);
+            }
+        }
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            const uint32_t pos = osp_pad(wo[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu));
+            const uint32_t pos = osp_pad(wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu));
             sm.keys[pos] = kB[j];
             if constexpr (KV) sm.vals[pos] = vB[j];
         }
         __syncthreads();  // (4) B reordered in LDS
-        OSP_T(8, 0);  // reorder
-        if (ST4) {  // slots 4 (g BLK + tid) + q, q = 0..3 (never across a pad word)
+        if constexpr (ST4) {  // slots 4 (g BLK + tid) + q, q = 0..3 (never across a pad word)
 #pragma unroll
             for (int g = 0; g < KPT / 4; ++g)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t at = osp_pad(4u * ((uint32_t)g * BLK + tid) + (uint32_t)q);
-                    kA[4 * g + q] = sm.keys[at];
-                    if constexpr (KV) vA[4 * g + q] = sm.vals[at];
-                }
-        } else if (!OSP_LDS_SCATTER) {
+                for (int q = 0; q < 4; ++q) kA[4 * g + q] = sm.keys[osp_pad(4u * ((uint32_t)g * BLK + tid) + (uint32_t)q)];
+        } else {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * BLK + tid)];
-        }
-        if constexpr (KV && !LDSV && !ST4) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) vA[j] = sm.vals[osp_pad(j * BLK + tid)];
+            for (int j = 0; j < KPT; ++j) {
+                kA[j] = sm.keys[osp_pad(j * BLK + tid)];
+                if constexpr (KV) vA[j] = sm.vals[osp_pad(j * BLK + tid)];
+            }
         }
         // each wave clears its own counters (no barrier before the next ranking)
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
-        OSP_T(9, 2);  // readback
         slotA = slotB;
         loA = loB;
         segA = segB;
         nvalidA = nvalidB;
         aggA = hB;
-        if constexpr (TWO_BAR || W0) {  // B's histogram and digit starts, from wave 0 (before barrier 4)
-            if (tid < (uint32_t)R) {
-                aggA = sm.agg[tid];
-                dstartA = sm.dst0[tid];
-            }
-        }
-        if constexpr (PF) {
+        if constexpr (GATHER) {
+            cB = cC;
+            cC = cD;
+            cD = sm.next;
+            e0D = e0N;
+            e1D = e1N;
+            sc ^= 1u;
+        } else if constexpr (PF) {
             cB = cC;
             cC = sm.next;
         } else {
             cB = sm.next;
         }
     }
-    if (JC && jnext != NEXT_NONE) {
-        __syncthreads();
-        const uint32_t rot = (blockIdx.x * 64u) & 4095u;
-        for (uint32_t i0 = tid; i0 < 4096u; i0 += BLK) {
-            const uint32_t i = (i0 + rot) & 4095u, c = sm.jh[i];
-            if (c) atomicAdd(jout + i, c);
-        }
-    }
-#ifndef LABSORT_OSP_TAILWB
-#define LABSORT_OSP_TAILWB 0
-#endif
-    // LABSORT_OSP_TAILWB (experiment): a workgroup out of tiles releases at agent scope,
-    // so its XCD's L2 starts writing back dirty lines while other workgroups still run,
-    // instead of all of it at the kernel-end release (the ~10 us between passes)
-    if constexpr (LABSORT_OSP_TAILWB != 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-#ifdef OSP_STAMPS
-    if (lane == 0)
-        for (int i = 0; i < 10; ++i) atomicAdd(&g_osp_stamps[i], st_[i]);
-    if (tid == 0) atomicAdd(&g_osp_stamps[10], 1ull);
-    if (tid == 0) {
-        atomicAdd(&g_osp_stamps[11], lbr_);
-        atomicAdd(&g_osp_stamps[12], lbs_);
-        atomicAdd(&g_osp_stamps[13], lbw_);
-        atomicAdd(&g_osp_stamps[14], lbt_);
-    }
-#endif
 }
 
 // ---------------------------------------------------------------------------------
@@ -1464,7 +1341,6 @@ struct TsSmem {
     uint32_t keys[TILE];
     uint32_t vals[KV ? TILE : 1];  // key/value: the payload follows its key through every pass
     uint32_t whist[W * R];
-    uint32_t dstart[R];
     uint32_t wsum[W];
     uint32_t red_and[W];
     uint32_t red_or[W];
@@ -1472,216 +1348,151 @@ struct TsSmem {
     uint32_t ordered;
 };
 
-// KV: key/value pairs (vin/vout, 4-byte payloads); the sort is stable, so equal keys
-// keep their input order and their payloads with them.
-// TS_PERSIST: one workgroup per CU loops over tiles (grid = CUs), so a tile's stores
-// drain while the next tile loads; TS_PFK > 0 also loads the first TS_PFK keys per
-// lane of the workgroup's next tile before its current tile's last pass.
-#ifndef LABSORT_TS_PERSIST
-#define LABSORT_TS_PERSIST 0
-#endif
-#ifndef LABSORT_TS_PFK
-#define LABSORT_TS_PFK 0
-#endif
+// One TILE-key tile per workgroup, sorted by up to four 8-bit LSD passes in LDS (passes
+// whose digit is uniform over the tile are skipped: the reference's "stop when sorted",
+// lab.cu:61, per tile).  KV: key/value pairs (vin/vout, 4-byte payloads); the sort is
+// stable, so equal keys keep their input order and their payloads with them.
+// Measured and not kept (r26): a persistent grid, the next tile's keys
+// loaded before the last pass, 16-B grouped loads and stores.
 template <int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint32_t *out, const uint32_t *vin,
                                                          uint32_t *vout, uint32_t n, uint32_t flip) {
     using S = TsSmem<BLOCK, KPT, KV>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE;
-    constexpr int PFK = KV ? 0 : (LABSORT_TS_PFK < KPT ? LABSORT_TS_PFK : KPT);
-#ifndef LABSORT_TS_V4
-#define LABSORT_TS_V4 0
-#endif
-    constexpr bool V4 = LABSORT_TS_V4 && !KV && PFK == 0 && KPT % 4 == 0;
     __shared__ S sm;
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t sentinel = ~flip;
-    const uint32_t ntiles = (n + (uint32_t)TILE - 1u) / (uint32_t)TILE;
     if (wid == 0) {  // lane-ordered LDS atomics (see k_onesweep_p): rank by one atomic per key
         const bool ord = lds_lane_ordered(sm.probe, lane);
         if (lane == 0) sm.ordered = ord ? 1u : 0u;
     }
-    uint32_t pf[PFK ? PFK : 1];
-    bool have_pf = false;
-    for (uint32_t tb = blockIdx.x; tb < ntiles; tb += gridDim.x) {
-        const uint32_t base = tb * (uint32_t)TILE;
-        const uint32_t wbase = base + wid * (KPT * WAVE) + lane;
-        uint32_t k[KPT];
-        uint32_t v[KV ? KPT : 1];
-        uint32_t a = ~0u, o = 0u;
-        const bool full = base + (uint32_t)TILE <= n;  // no bounds checks (one base address)
-        const bool g4 = V4 && full && ((((uintptr_t)in) | ((uintptr_t)out)) & 15u) == 0u;  // grouped 16-B I/O
-        if constexpr (KV) {
+    const uint32_t base = blockIdx.x * (uint32_t)TILE;
+    const uint32_t wbase = base + wid * (KPT * WAVE) + lane;
+    uint32_t k[KPT];
+    uint32_t v[KV ? KPT : 1];
+    uint32_t a = ~0u, o = 0u;
+    const bool full = base + (uint32_t)TILE <= n;
+    if constexpr (KV) {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t idx = wbase + j * WAVE;
-                v[j] = idx < n ? vin[idx] : 0u;
-            }
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            v[j] = idx < n ? vin[idx] : 0u;
         }
-        // V4 (keys only, full tiles): 16-B loads, each lane 4 consecutive keys per 256-key
-        // chunk ("grouped" order: the first pass may rank equal digits in any order), and
-        // after the last pass a grouped read-back, so the tile leaves as 16-B stores
-        const uint32_t gbase = base + wid * (KPT * WAVE) + 4u * lane;  // + 256 q + s
-        if (g4) {
+    }
+    if (full) {
 #pragma unroll
-            for (int q = 0; q < KPT / 4; ++q) {
-                const uint4 x = *reinterpret_cast<const uint4 *>(in + gbase + 256u * q);
-                k[4 * q] = x.x;
-                k[4 * q + 1] = x.y;
-                k[4 * q + 2] = x.z;
-                k[4 * q + 3] = x.w;
-            }
+        for (int j = 0; j < KPT; ++j) k[j] = ld_stream<NT_TILE>(in + wbase + j * WAVE);
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                a &= k[j] ^ flip;
-                o |= k[j] ^ flip;
-            }
-        } else if (full) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j)
-                k[j] = (j < PFK && have_pf) ? pf[j < PFK ? j : 0] : ld_stream<NT_TILE>(in + wbase + j * WAVE);
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                a &= k[j] ^ flip;
-                o |= k[j] ^ flip;
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t idx = wbase + j * WAVE;
-                const bool ok = idx < n;
-                k[j] = ok ? ld_stream<NT_TILE>(in + idx) : sentinel;
-                const uint32_t x = k[j] ^ flip;
-                a &= ok ? x : ~0u;
-                o |= ok ? x : 0u;
-            }
+        for (int j = 0; j < KPT; ++j) {
+            a &= k[j] ^ flip;
+            o |= k[j] ^ flip;
         }
-        have_pf = false;
-        // bits on which the tile's keys differ -> passes that are not the identity
+    } else {
 #pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            a &= __shfl_xor(a, off);
-            o |= __shfl_xor(o, off);
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            const bool ok = idx < n;
+            k[j] = ok ? ld_stream<NT_TILE>(in + idx) : sentinel;
+            const uint32_t x = k[j] ^ flip;
+            a &= ok ? x : ~0u;
+            o |= ok ? x : 0u;
         }
-        if (lane == 0) {
-            sm.red_and[wid] = a;
-            sm.red_or[wid] = o;
+    }
+    // bits on which the tile's keys differ -> passes that are not the identity
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        a &= __shfl_xor(a, off);
+        o |= __shfl_xor(o, off);
+    }
+    if (lane == 0) {
+        sm.red_and[wid] = a;
+        sm.red_or[wid] = o;
+    }
+    __syncthreads();
+    const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
+    uint32_t diff = 0;
+    {
+        uint32_t aa = ~0u, oo = 0u;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            aa &= sm.red_and[w];
+            oo |= sm.red_or[w];
+        }
+        diff = aa ^ oo;
+    }
+    uint32_t *wh = sm.whist + wid * R;
+    for (int pass = 0; pass < 4; ++pass) {
+        const uint32_t shift = pass * 8;
+        if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the tile
+        for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
+        uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            // stable wave rank: lane-ordered returning atomic, else peers by 8 ballots
+            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+            uint32_t r;
+            if (atomic_rank) {
+                r = wave_atomic_rank(wh, d, lane);
+            } else {
+                const uint64_t m = match8(d);
+                const uint32_t pre = mbcnt64(m);
+                const uint32_t old = wh[d];
+                if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
+                r = old + pre;
+            }
+            rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
         }
         __syncthreads();
-        const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
-        uint32_t diff = 0;
-        {
-            uint32_t aa = ~0u, oo = 0u;
+        // tile-wide digit offsets folded into the per-wave offsets: the reorder then
+        // reads one LDS word per key instead of two (r17)
+        uint32_t tot = 0;
+        if (tid < (uint32_t)R) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) tot += sm.whist[w * R + tid];
+        }
+        const uint32_t ds = block_excl_scan<BLOCK, R>(tot, sm.wsum);
+        if (tid < (uint32_t)R) {
+            uint32_t run = ds;
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-                aa &= sm.red_and[w];
-                oo |= sm.red_or[w];
-            }
-            diff = aa ^ oo;
-        }
-        // next tile of this workgroup (persistent grid), prefetched before the last pass
-        const uint32_t tn = tb + gridDim.x;
-        const bool pf_next = PFK > 0 && tn < n / (uint32_t)TILE;  // the next tile is a full one
-        const int last = diff ? (31 - __builtin_clz(diff)) / 8 : -1;
-        uint32_t *wh = sm.whist + wid * R;
-        for (int pass = 0; pass < 4; ++pass) {
-            const uint32_t shift = pass * 8;
-            if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the block
-            if (PFK > 0 && pf_next && pass == last) {
-                const uint32_t nb = tn * (uint32_t)TILE + wid * (KPT * WAVE) + lane;
-#pragma unroll
-                for (int j = 0; j < PFK; ++j) pf[j] = ld_stream<NT_TILE>(in + nb + j * WAVE);
-                have_pf = true;
-            }
-            for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
-            uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                // stable wave rank: lane-ordered returning atomic, else peers by 8 ballots
-                const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-                uint32_t r;
-                if (atomic_rank) {
-                    r = wave_atomic_rank(wh, d, lane);
-                } else {
-                    const uint64_t m = match8(d);
-                    const uint32_t pre = mbcnt64(m);
-                    const uint32_t old = wh[d];
-                    if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
-                    r = old + pre;
-                }
-                rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
-            }
-            __syncthreads();
-            // tile-wide digit offsets folded into the per-wave offsets: the reorder then
-            // reads one LDS word per key instead of two (LDS was busy 68 % of the kernel,
-            // 60 % of it bank conflicts: profiles/r17_pmc_tile_sort.txt)
-            uint32_t tot = 0;
-            if (tid < (uint32_t)R) {
-#pragma unroll
-                for (int w = 0; w < W; ++w) tot += sm.whist[w * R + tid];
-            }
-            const uint32_t ds = block_excl_scan<BLOCK, R>(tot, sm.wsum);
-            if (tid < (uint32_t)R) {
-                uint32_t run = ds;
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    const uint32_t c = sm.whist[w * R + tid];
-                    sm.whist[w * R + tid] = run;
-                    run += c;
-                }
-            }
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-                const uint32_t dst = wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
-                sm.keys[dst] = k[j];
-                if constexpr (KV) sm.vals[dst] = v[j];
-            }
-            __syncthreads();
-            if (g4 && pass == last) {  // grouped read-back (16-B LDS reads, conflict-free)
-#pragma unroll
-                for (int q = 0; q < KPT / 4; ++q) {
-                    const uint4 x = *reinterpret_cast<const uint4 *>(sm.keys + wid * (KPT * WAVE) + 4u * lane + 256u * q);
-                    k[4 * q] = x.x;
-                    k[4 * q + 1] = x.y;
-                    k[4 * q + 2] = x.z;
-                    k[4 * q + 3] = x.w;
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
-            }
-            if constexpr (KV) {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) v[j] = sm.vals[wid * (KPT * WAVE) + j * WAVE + lane];
+                const uint32_t c = sm.whist[w * R + tid];
+                sm.whist[w * R + tid] = run;
+                run += c;
             }
         }
-        if (g4) {
+        __syncthreads();
 #pragma unroll
-            for (int q = 0; q < KPT / 4; ++q)
-                *reinterpret_cast<uint4 *>(out + gbase + 256u * q) = make_uint4(k[4 * q], k[4 * q + 1], k[4 * q + 2], k[4 * q + 3]);
-        } else if (full) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
-        } else {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t idx = wbase + j * WAVE;
-                if (idx < n) out[idx] = k[j];
-            }
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+            const uint32_t dst = wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
+            sm.keys[dst] = k[j];
+            if constexpr (KV) sm.vals[dst] = v[j];
         }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = sm.keys[wid * (KPT * WAVE) + j * WAVE + lane];
         if constexpr (KV) {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                const uint32_t idx = wbase + j * WAVE;
-                if (idx < n) vout[idx] = v[j];
-            }
+            for (int j = 0; j < KPT; ++j) v[j] = sm.vals[wid * (KPT * WAVE) + j * WAVE + lane];
         }
-        // a uniform tile runs no pass barrier: keep the next tile's red_and/red_or writes
-        // behind every wave's reads of this tile's
-        if (!LABSORT_TS_PERSIST) break;  // one tile per workgroup
-        if (diff == 0u) __syncthreads();
+        // (the next pass's reorder writes sm.keys two barriers later)
+    }
+    if (full) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
+    } else {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            if (idx < n) out[idx] = k[j];
+        }
+    }
+    if constexpr (KV) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            if (idx < n) vout[idx] = v[j];
+        }
     }
 }
 
@@ -1724,35 +1535,6 @@ __device__ __forceinline__ uint32_t corank(const uint32_t *A, uint32_t la, const
         const uint32_t mid = (lo + hi) >> 1;
         if (key_le(A[mid], B[diag - 1u - mid], flip)) lo = mid + 1u;
         else hi = mid;
-    }
-    return lo;
-}
-
-// The same co-rank by a group of K consecutive lanes (K divides 64): each round the
-// group probes K points of [lo, hi) at once and keeps the interval between the last
-// probe where A's key goes first and the next one, so a search over 2^27 keys takes
-// 5 dependent rounds of loads at K = 64 (4 at K = 16 over a 32K-key bracket) instead
-// of 27.  Every lane of the wave calls it (ballots); `live`: this group searches.
-template <int K>
-__device__ __forceinline__ uint32_t corank_group(const uint32_t *A, uint32_t la, const uint32_t *B, uint32_t lb,
-                                                 uint32_t diag, uint32_t flip, uint32_t lo, uint32_t hi, bool live) {
-    const uint32_t lane = threadIdx.x & 63u, sub = lane & (uint32_t)(K - 1), gbase = lane & ~(uint32_t)(K - 1);
-    if (diag > lb && lo < diag - lb) lo = diag - lb;
-    if (hi > diag) hi = diag;
-    if (hi > la) hi = la;
-    if (!live) lo = hi = 0u;
-    while (__ballot(lo < hi) != 0ull) {
-        const uint32_t span = hi - lo;
-        const uint32_t p = lo + (uint32_t)(((uint64_t)(sub + 1u) * span) / (uint64_t)(K + 1));
-        const bool pred = lo < hi && key_le(A[p], B[diag - 1u - p], flip);
-        const uint64_t bal = __ballot(pred) >> gbase;
-        const uint32_t c = (uint32_t)__popcll(K == 64 ? bal : (bal & ((1ull << (K & 63)) - 1ull)));
-        if (lo < hi) {  // the probes' predicate is true on a prefix of them (c probes)
-            const uint32_t nlo = c ? lo + (uint32_t)(((uint64_t)c * span) / (uint64_t)(K + 1)) + 1u : lo;
-            const uint32_t nhi = c < (uint32_t)K ? lo + (uint32_t)(((uint64_t)(c + 1u) * span) / (uint64_t)(K + 1)) : hi;
-            lo = nlo;
-            hi = nhi;
-        }
     }
     return lo;
 }
@@ -1873,60 +1655,12 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         }
         return corank(src + g.pb, g.la, src + g.pb + g.la, g.lb, o - g.pb, flip, lo, hi);
     };
-    if constexpr (MG_KARY) {
-        // the same two rounds with lane-group searches: round 1 one wave per co-rank (64
-        // probes per load round), round 2 one 16-lane group per co-rank inside its bracket
-        auto group_search = [&](uint32_t i, uint32_t S, bool live, auto kc) {
-            constexpr int K = decltype(kc)::value;
-            const uint32_t o = (t0 + i) * T;
-            live = live && o < n;
-            const PairGeom g = live ? pair_of(o, n, run, pr) : PairGeom{0u, 0u, 0u};
-            uint32_t lo = 0u, hi = ~0u;
-            if (live && S) {
-                const uint32_t il = i - i % S, ih = il + S < nb ? il + S : nb;
-                const uint32_t ol = (t0 + il) * T, oh = (t0 + ih) * T;
-                if (pair_of(ol, n, run, pr).pb == g.pb) {
-                    lo = s_part[il];
-                    hi = lo + (o - ol);
-                }
-                if (oh < n && pair_of(oh, n, run, pr).pb == g.pb) {
-                    const uint32_t ah = s_part[ih];
-                    hi = hi < ah ? hi : ah;
-                    if (ah > oh - o && lo < ah - (oh - o)) lo = ah - (oh - o);
-                }
-            }
-            return corank_group<K>(src + g.pb, g.la, src + g.pb + g.la, g.lb, live ? o - g.pb : 0u, flip, lo, hi, live);
-        };
-        constexpr uint32_t NWV = BLOCK / MG_K1, NG = BLOCK / MG_K2;  // round 1 / round 2 searches at once
-        const uint32_t wv = tid / MG_K1, lane = tid & 63u;
-        const uint32_t r1 = nb / MG_BRACKET + 1u + (nb % MG_BRACKET ? 1u : 0u);  // i = 0, S, 2S, ... and nb
-        for (uint32_t k = 0; k * NWV < r1; ++k) {
-            const uint32_t e = k * NWV + wv;
-            const uint32_t i = e * MG_BRACKET <= nb ? e * MG_BRACKET : nb;
-            const uint32_t a = group_search(i, 0u, e < r1, std::integral_constant<int, MG_K1>{});
-            if (e < r1 && lane % MG_K1 == 0u) s_part[i] = a;
-        }
-        __syncthreads();
-        for (uint32_t k = 0; k * NG < nb; ++k) {
-            const uint32_t i = k * NG + tid / MG_K2;
-            const uint32_t a = group_search(i, MG_BRACKET, i < nb && (i % MG_BRACKET) != 0u, std::integral_constant<int, MG_K2>{});
-            if (i < nb && (i % MG_BRACKET) != 0u && tid % MG_K2 == 0u) s_part[i] = a;
-        }
-        __syncthreads();
-    } else {
-        for (uint32_t i = tid * MG_BRACKET; i <= nb; i += BLOCK * MG_BRACKET) s_part[i] = search(i, 0);
-        if (tid == 0 && nb % MG_BRACKET) s_part[nb] = search(nb, 0);
-        __syncthreads();
-        for (uint32_t i = tid; i < nb; i += BLOCK)
-            if (i % MG_BRACKET) s_part[i] = search(i, MG_BRACKET);
-        __syncthreads();
-    }
-#ifdef LABSORT_MG_DIAG_PROLOGUE
-    if (LABSORT_MG_DIAG_PROLOGUE == 1 || (LABSORT_MG_DIAG_PROLOGUE == 2 && n == 0xFFFFFFFFu)) {  // timing build: co-ranks only
-        if (tid == 0 && s_part[0] == 0xFFFFFFFFu) dst[0] = 0u;
-        return;
-    }
-#endif
+    for (uint32_t i = tid * MG_BRACKET; i <= nb; i += BLOCK * MG_BRACKET) s_part[i] = search(i, 0);
+    if (tid == 0 && nb % MG_BRACKET) s_part[nb] = search(nb, 0);
+    __syncthreads();
+    for (uint32_t i = tid; i < nb; i += BLOCK)
+        if (i % MG_BRACKET) s_part[i] = search(i, MG_BRACKET);
+    __syncthreads();
     struct Geo {
         uint32_t o0, tot, la, sa, sb;  // output start, keys, A keys, A start, B start (absolute)
     };
@@ -1944,36 +1678,7 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         q.sb = g.pb + g.la + b0;
         return q;
     };
-#ifndef LABSORT_MG_LD4
-#define LABSORT_MG_LD4 0
-#endif
-    // LD4: thread keeps tile slots 4 (j BLOCK/4 + tid) + q, loaded as one 16-B load when the
-    // four lie in one run (A or B) and the tile (else four 4-B loads)
-    constexpr bool LD4 = LABSORT_MG_LD4 && !KV && KPT % 4 == 0;
     auto load = [&](const Geo &q, uint32_t (&v)[KPT], uint32_t (&vv)[KV ? KPT : 1]) {
-        if constexpr (LD4) {
-#pragma unroll
-            for (int j = 0; j < KPT / 4; ++j) {
-                const uint32_t k0 = 4u * (tid + (uint32_t)j * BLOCK);
-                if (k0 + 3u < q.tot && (k0 + 3u < q.la || k0 >= q.la)) {
-                    const uint32_t a = k0 < q.la ? q.sa + k0 : q.sb + (k0 - q.la);
-                    uint32_t w[4];
-                    __builtin_memcpy(w, src + a, 16);  // (4-B aligned: one 16-B load)
-                    v[4 * j] = w[0];
-                    v[4 * j + 1] = w[1];
-                    v[4 * j + 2] = w[2];
-                    v[4 * j + 3] = w[3];
-                } else {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const uint32_t k = k0 + (uint32_t)u;
-                        const uint32_t a = k < q.la ? q.sa + k : q.sb + (k - q.la);
-                        v[4 * j + u] = k < q.tot ? src[a] : 0u;
-                    }
-                }
-            }
-            return;
-        }
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t k = tid + (uint32_t)j * BLOCK;
@@ -1988,15 +1693,8 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
     load(cur, nx, nv);
     for (uint32_t t = t0; t < t1; ++t) {
         __syncthreads();  // previous tile's merge no longer reads sm.in
-        if constexpr (LD4) {
 #pragma unroll
-            for (int j = 0; j < KPT / 4; ++j)
-                *reinterpret_cast<uint4 *>(sm.in + 4u * (tid + (uint32_t)j * BLOCK)) =
-                    make_uint4(nx[4 * j], nx[4 * j + 1], nx[4 * j + 2], nx[4 * j + 3]);
-        } else {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
-        }
+        for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
         if constexpr (KV) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) sm.vin[tid + (uint32_t)j * BLOCK] = nv[j];
@@ -2030,10 +1728,7 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
                 vb = bi < lb ? sb[bi] : 0u;
             }
         }
-#ifndef LABSORT_MG_DIRECT
-#define LABSORT_MG_DIRECT 1
-#endif
-        if (!KV && LABSORT_MG_DIRECT && KPT % 4 == 0 && tot == T && (((uintptr_t)dst) & 15u) == 0) {
+        if (!KV && KPT % 4 == 0 && tot == T && (((uintptr_t)dst) & 15u) == 0) {
             // a full tile: each thread's KPT outputs are consecutive, so they go straight
             // to HBM as KPT/4 16-B stores (no LDS staging round trip, one barrier fewer)
             uint4 *o4 = reinterpret_cast<uint4 *>(dst + cur.o0 + tid * KPT);
@@ -2091,6 +1786,30 @@ __global__ __launch_bounds__(BLOCK) void k_merge_ab(const uint32_t *__restrict__
     const uint32_t o1 = (d1 - o0) < (uint32_t)MG_TILE ? d1 : o0 + (uint32_t)MG_TILE;
     const uint32_t a0 = part[i], a1 = part[i + 1];
     merge_tile<BLOCK, KPT>(A, a0, a1, B, o0 - a0, o1 - a1, out + (o0 - d0), flip, sm);
+}
+
+// ---------------------------------------------------------------------------------
+// streaming copy: the practical ceiling of a read-once / write-once pass (bench.py's
+// copy_ceiling).  16384-word tiles per 1024-thread workgroup, 4 x 16 B per lane,
+// nontemporal loads and stores, persistent grid of one workgroup per CU (the layout of
+// harness/exp/lsweep_probe.hip's fastest copy: 0.389 ms for 2^28 words, 5.5 TB/s).
+// ---------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_stream_copy(const u32x4 *__restrict__ a, u32x4 *__restrict__ b, size_t n4) {
+    const size_t ntiles = n4 / 4096;
+    const uint32_t tid = threadIdx.x;
+    for (size_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        const u32x4 *s = a + t * 4096 + tid;
+        u32x4 k[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) k[j] = __builtin_nontemporal_load(s + j * 1024);
+        u32x4 *d = b + t * 4096 + tid;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) __builtin_nontemporal_store(k[j], d + j * 1024);
+    }
+    for (size_t i = ntiles * 4096 + (size_t)blockIdx.x * 1024 + tid; i < n4; i += (size_t)gridDim.x * 1024) b[i] = a[i];
+}
+__global__ __launch_bounds__(256) void k_word_copy(const uint32_t *__restrict__ a, uint32_t *__restrict__ b, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) b[i] = a[i];
 }
 
 // ---------------------------------------------------------------------------------
@@ -2167,20 +1886,11 @@ hipError_t launch_plan(const uint32_t *hist, size_t n, int bits, int in_is_out, 
 
 hipError_t launch_onesweep(Bufs b, const Plan *plan, int pass, int bits, size_t n, uint32_t flip,
                            const uint32_t *hist, uint32_t *lookback, uint32_t *counter, uint32_t *err,
-                           hipStream_t s, const Bufs *vb) {
+                           hipStream_t s) {
+    if (bits != 1) return hipErrorInvalidValue;  // 8-bit digits: the persistent pass
     const unsigned g = (unsigned)((n + OS_TILE - 1) / OS_TILE);
-    if (vb && bits == 8)
-        k_onesweep<8, OS_BLOCK, OS_KPT, true><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist,
-                                                                     lookback, counter, err, *vb);
-    else if (vb)
-        return hipErrorInvalidValue;
-    else if (bits == 8)
-        k_onesweep<8, OS_BLOCK, OS_KPT><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback,
-                                                               counter, err, Bufs{});
-    else if (bits == 1)
-        k_onesweep<1, OS_BLOCK, OS_KPT><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback,
-                                                               counter, err, Bufs{});
-    else return hipErrorInvalidValue;
+    k_onesweep<1, OS_BLOCK, OS_KPT><<<g, OS_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, hist, lookback, counter,
+                                                           err);
     return hipGetLastError();
 }
 
@@ -2196,32 +1906,19 @@ static int cu_count() {
 
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
                              uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s, const Bufs *vb,
-                             uint32_t *jout) {
+                             const GthTables *tb) {
     const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE + NSEG;
-    const size_t want = (size_t)OSP_BLOCKS_PER_CU * cu_count();
+    const size_t want = (size_t)cu_count();  // one workgroup per CU (LDS-bound)
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
-    static int variant = -1;
-    if (variant < 0) {  // LABSORT_OSP=<rank 0/1/2><hist first 0/1>; default OSP_DEFAULT_VARIANT
-        const char *e = std::getenv("LABSORT_OSP");
-        variant = (e && e[0] >= '0' && e[0] <= '2' && e[1]) ? ((e[0] - '0') << 1) | (e[1] == '1') : OSP_DEFAULT_VARIANT;
-    }
-    if (vb) {  // key/value: the default variant (lane-ordered atomic rank) only
-        if constexpr (OSP_TILE <= 16384) {  // keys + payloads in LDS: 16384-pair tiles at most
-            k_onesweep_p<2, false, true><<<g, OSP_KV_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback,
-                                                                 counter, err, *vb);
-            return hipGetLastError();
-        }
-        return hipErrorInvalidValue;
-    }
-    switch (variant) {
-    case 0: k_onesweep_p<0, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
-    case 1: k_onesweep_p<0, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
-    case 2: k_onesweep_p<1, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
-    case 3: k_onesweep_p<1, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
-    case 4: k_onesweep_p<2, false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b, jout); break;
-    case 5: k_onesweep_p<2, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b); break;
-    default: return hipErrorInvalidValue;
-    }
+    if (vb)
+        k_onesweep_p<true><<<g, OSP_KV_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, *vb,
+                                                     GthTables{});
+    else if (tb)
+        k_onesweep_p<false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err,
+                                                          b, *tb);
+    else
+        k_onesweep_p<false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b,
+                                                    GthTables{});
     return hipGetLastError();
 }
 
@@ -2237,37 +1934,17 @@ hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32
     return hipGetLastError();
 }
 
-// Look-back chains per pass (LABSORT_SEG, read once per process):
-//   "on" (default, OSP_SEG_LATER = 1): NSEG position segments in the first active
-//            pass, digit-group segments in the later passes (joint histograms
-//            counted by k_hist_seg);
-//   "first": position segments in the first active pass, one chain in the later
-//            passes;
-//   "none":  one chain in every pass.
-// Measured on MI355X at 2^28: with XCD-grouped acquisition the digit-group segments
-// gain ~4 % over one chain in the later passes (r13 -> r14); without it (r09) one
-// chain was 1-2 % faster.
-static int seg_later() {
-    static int v = 2;
-    if (v == 2) {
-        const char *e = std::getenv("LABSORT_SEG");
-        v = !e ? OSP_SEG_LATER : std::strcmp(e, "on") == 0 ? 1 : std::strcmp(e, "none") == 0 ? -1 : 0;
-    }
-    return v;
-}
-
 hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, int in_is_out, Plan *plan,
                         SegPlan *segplans, uint32_t *hist, void *zero_p, size_t zero_bytes, hipStream_t s) {
-    // LABSORT_PLAN_ZERO=0: the look-back clear as its own k_zero launch (A/B)
-    const char *e = std::getenv("LABSORT_PLAN_ZERO");
-    const bool fold = !(e && e[0] == '0') && zero_bytes % 16 == 0;
+    // the look-back clear rides in the plan launch (workgroups 1..): one launch fewer (r27)
+    const bool fold = zero_bytes % 16 == 0;
     if (!fold && zero_bytes) {
         const hipError_t z = launch_zero(zero_p, zero_bytes, s);
         if (z != hipSuccess) return z;
     }
     const size_t zn4 = fold ? zero_bytes / 16 : 0;
     const unsigned g = 1u + (zn4 ? blocks_for(zn4, 256 * 4, 2048) : 0u);
-    k_plan8<<<g, 256, 0, s>>>(hps, joint, (uint32_t)n, in_is_out, seg_later(), plan, segplans, hist,
+    k_plan8<<<g, 256, 0, s>>>(hps, joint, (uint32_t)n, in_is_out, 1, plan, segplans, hist,
                               static_cast<uint4 *>(zero_p), zn4);
     return hipGetLastError();
 }
@@ -2300,8 +1977,7 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) 
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t nt = (n + TS_TILE - 1) / TS_TILE;
-    const unsigned g = (unsigned)(LABSORT_TS_PERSIST && nt > (size_t)cu_count() ? (size_t)cu_count() : nt);
-    k_tile_sort<TS_BLOCK, TS_KPT><<<g, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
+    k_tile_sort<TS_BLOCK, TS_KPT><<<(unsigned)nt, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
     return hipGetLastError();
 }
 
@@ -2358,6 +2034,18 @@ hipError_t launch_upper_bound(const uint32_t *keys, size_t n, uint32_t flip, con
     return hipGetLastError();
 }
 
+hipError_t launch_stream_copy(const uint32_t *in, uint32_t *out, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    if (((((uintptr_t)in) | ((uintptr_t)out)) & 15u) == 0) {
+        const size_t n4 = n / 4;
+        if (n4) k_stream_copy<<<(unsigned)cu_count(), 1024, 0, s>>>(reinterpret_cast<const u32x4 *>(in), reinterpret_cast<u32x4 *>(out), n4);
+        if (n % 4) k_word_copy<<<1, 256, 0, s>>>(in + n4 * 4, out + n4 * 4, n % 4);
+    } else {
+        k_word_copy<<<blocks_for(n, 256 * 16, 4096), 256, 0, s>>>(in, out, n);
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_count_descents(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *count, hipStream_t s) {
     if (n < 2) return hipSuccess;
     k_count_descents<<<blocks_for(n, 256 * 16, 4096), 256, 0, s>>>(keys, n, flip, count);
@@ -2366,13 +2054,3 @@ hipError_t launch_count_descents(const uint32_t *keys, size_t n, uint32_t flip, 
 
 }  // namespace labsort
 
-#ifdef OSP_STAMPS
-extern "C" int labsort_exp_stamps(unsigned long long *host16, int reset) {
-    if (hipMemcpyFromSymbol(host16, HIP_SYMBOL(labsort::g_osp_stamps), 16 * 8) != hipSuccess) return 2;
-    if (reset) {
-        unsigned long long z[16] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(labsort::g_osp_stamps), z, sizeof z) != hipSuccess) return 2;
-    }
-    return 0;
-}
-#endif

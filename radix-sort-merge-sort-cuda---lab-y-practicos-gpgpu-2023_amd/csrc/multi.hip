@@ -288,9 +288,8 @@ struct HipRankOps {
                 MHIP(hipMemcpyAsync(O + b, recv + b, (e - b) * 4, hipMemcpyDeviceToDevice, s));
                 return LABSORT_OK;
             }
-            size_t o[LABSORT_MULTI_MAX_RANKS + 1];
-            for (int q = q0; q <= q1; ++q) o[q - q0] = offs[q];
-            LCALL(labsort_merge_runs(recv, O, o, q1 - q0, key_type, R.mws.p, R.mws.bytes, s));
+            std::vector<size_t> o(offs + q0, offs + q1 + 1);  // (q1 - q0 <= 8: LABSORT_DIST_MAX_RANKS)
+            LCALL(labsort_merge_runs(recv, O, o.data(), q1 - q0, key_type, R.mws.p, R.mws.bytes, s));
             return LABSORT_OK;
         };
         int st;
@@ -327,8 +326,9 @@ struct HipRankOps {
         return LABSORT_OK;
     }
 
-    // phases (ms, device timeline) of the call just finished
-    void phases(double *ph, bool host) {
+    // phases (ms, device timeline) of the call just finished; the plan's work and wait from
+    // the host times at its collectives
+    void phases(double *ph, bool host, const dist::Result &res) {
         auto el = [&](hipEvent_t a, hipEvent_t b) {
             float ms = 0.f;
             return hipEventElapsedTime(&ms, a, b) == hipSuccess ? (double)ms : 0.0;
@@ -339,6 +339,11 @@ struct HipRankOps {
         ph[3] = el(R.tev[dist::M_PLANNED], R.tev[dist::M_EXCHANGED]);
         ph[4] = el(R.tev[dist::M_EXCHANGED], R.tev[dist::M_MERGED]);
         ph[5] = host ? el(R.tev[dist::M_MERGED], R.tev[EV_D2H]) : 0.0;
+        double wait = 0.0;
+        for (int k = 0; k < dist::C_NCOLL; ++k)
+            if (res.arrive[k] >= 0.0) wait += res.leave[k] - res.arrive[k];
+        ph[8] = wait;
+        ph[7] = ph[2] > wait ? ph[2] - wait : 0.0;
     }
 };
 
@@ -436,10 +441,11 @@ struct ThreadShared {
     std::vector<ncclComm_t> comms;         // RCCL transport: one communicator per rank
     explicit ThreadShared(int n) : p(n), slot(n), rptr(n, nullptr), sent(n, nullptr), dev(n, -1) {}
 
-    // all ranks arrive; LABSORT_ERR_DEVICE if one of them failed (it never arrives)
+    // all ranks arrive; LABSORT_ERR_PEER if one of them failed without arriving (a rank
+    // that failed in its own step still arrives: the schedule's status words report it)
     int barrier() {
         std::unique_lock<std::mutex> lk(mu);
-        if (failed) return LABSORT_ERR_DEVICE;
+        if (failed) return LABSORT_ERR_PEER;
         const unsigned g = gen;
         if (++arrived == p) {
             arrived = 0;
@@ -448,7 +454,7 @@ struct ThreadShared {
             return LABSORT_OK;
         }
         cv.wait(lk, [&] { return gen != g || failed; });
-        return gen != g ? LABSORT_OK : LABSORT_ERR_DEVICE;
+        return gen != g ? LABSORT_OK : LABSORT_ERR_PEER;
     }
     void abort() {
         std::lock_guard<std::mutex> lk(mu);
@@ -572,6 +578,7 @@ std::vector<RankState> g_ranks;  // per rank slot, re-bound when its device chan
 std::vector<int> g_comm_devs;    // devices of the cached ncclCommInitAll communicators
 std::vector<ncclComm_t> g_comms;
 double g_phase_ms[LABSORT_MULTI_PHASES];
+std::vector<dist::Result> g_res;  // each rank's collective times in the last call
 size_t g_sent_bytes = 0;
 std::vector<size_t> g_range_counts;  // keys of each rank's range in the last call
 
@@ -657,7 +664,7 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
             const int f = ops.finish();  // drain the streams even after a failure
             if (!e) e = f;
             if (e) sh.abort();
-            else ops.phases(ph[r].data(), true);
+            else ops.phases(ph[r].data(), true, res[r]);
             st[r] = e;
             hip[r] = t_last_hip;
         });
@@ -668,23 +675,25 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
         (void)hipEventDestroy(sent_ev[r]);
     }
     if (pin) MHIP(hipHostUnregister(h));
-    // the first rank that failed for a reason of its own (others report the abort)
+    // the first rank that failed for a reason of its own (the others report its failure)
     for (int pass = 0; pass < 2; ++pass)
         for (int r = 0; r < p; ++r)
-            if (st[r] && (pass == 1 || st[r] != LABSORT_ERR_DEVICE || hip[r])) {
+            if (st[r] && (pass == 1 || st[r] != LABSORT_ERR_PEER)) {
                 t_last_hip = hip[r];
                 return st[r];
             }
     for (int i = 0; i < LABSORT_MULTI_PHASES; ++i) g_phase_ms[i] = 0.0;
     size_t sent = 0;
     for (int r = 0; r < p; ++r) {
-        for (int i = 0; i < 6; ++i) g_phase_ms[i] = std::max(g_phase_ms[i], ph[r][i]);
+        for (int i = 0; i < LABSORT_MULTI_PHASES; ++i)
+            if (i != 6) g_phase_ms[i] = std::max(g_phase_ms[i], ph[r][i]);
         sent = std::max(sent, (size_t)res[r].sent);
     }
     g_phase_ms[6] = t1 - t0;
     g_sent_bytes = sent;
     g_range_counts.assign(p, 0);
     for (int r = 0; r < p; ++r) g_range_counts[r] = (size_t)res[r].count;
+    g_res = res;
     return LABSORT_OK;
 }
 
@@ -703,6 +712,7 @@ struct labsort_comm {
     labsort::Buf stage;
     std::vector<uint32_t> hs, hr;
     double phase[LABSORT_MULTI_PHASES] = {};
+    labsort::dist::Result res;  // collective times of the last sort
     size_t sent = 0;
     int last_hip = 0;
 };
@@ -748,6 +758,18 @@ int labsort_multi_timing(double *phase_ms, int nphases, size_t *max_sent_bytes) 
     std::lock_guard<std::mutex> lk(g_mu);
     for (int i = 0; i < nphases; ++i) phase_ms[i] = g_phase_ms[i];
     if (max_sent_bytes) *max_sent_bytes = g_sent_bytes;
+    return LABSORT_OK;
+}
+
+int labsort_multi_collectives(double *arrive, double *leave, int nranks, int ncoll) {
+    if (!arrive || !leave || nranks < 0 || ncoll < 0 || ncoll > dist::C_NCOLL) return LABSORT_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if ((size_t)nranks > g_res.size()) return LABSORT_ERR_ARG;
+    for (int r = 0; r < nranks; ++r)
+        for (int k = 0; k < ncoll; ++k) {
+            arrive[r * ncoll + k] = g_res[r].arrive[k];
+            leave[r * ncoll + k] = g_res[r].leave[k];
+        }
     return LABSORT_OK;
 }
 
@@ -797,7 +819,8 @@ int labsort_comm_unique_id(void *id) {
 }
 
 int labsort_comm_init_rccl(labsort_comm_t *comm, const void *id, int nranks, int rank) {
-    if (!comm || !id || nranks < 1 || rank < 0 || rank >= nranks) return LABSORT_ERR_ARG;
+    if (!comm || !id || nranks < 1 || nranks > LABSORT_DIST_MAX_RANKS || rank < 0 || rank >= nranks)
+        return LABSORT_ERR_ARG;
     *comm = nullptr;
     if (!g_rccl.load()) return LABSORT_ERR_HIP;
     labsort_comm *c = new labsort_comm;
@@ -820,7 +843,8 @@ int labsort_comm_init_rccl(labsort_comm_t *comm, const void *id, int nranks, int
 }
 
 int labsort_comm_init_host(labsort_comm_t *comm, int nranks, int rank, const labsort_host_coll *coll) {
-    if (!comm || !coll || !coll->allgather || !coll->alltoallv || nranks < 1 || rank < 0 || rank >= nranks)
+    if (!comm || !coll || !coll->allgather || !coll->alltoallv || nranks < 1 || nranks > LABSORT_DIST_MAX_RANKS ||
+        rank < 0 || rank >= nranks)
         return LABSORT_ERR_ARG;
     labsort_comm *c = new labsort_comm;
     c->kind = 2;
@@ -883,8 +907,9 @@ int labsort_dist_sort(labsort_comm_t c, const void *d_keys, size_t m, int key_ty
     const int f = ops.finish();
     if (!st) st = f;
     c->last_hip = t_last_hip;
+    c->res = res;  // (collective times also after a failure)
     if (st) return st;
-    ops.phases(c->phase, false);
+    ops.phases(c->phase, false, res);
     c->phase[6] = now_ms() - t0;
     c->sent = res.sent;
     *d_result = res.data;
@@ -897,6 +922,15 @@ int labsort_dist_timing(labsort_comm_t c, double *phase_ms, int nphases, size_t 
     if (!c || !phase_ms || nphases < 0 || nphases > LABSORT_MULTI_PHASES) return LABSORT_ERR_ARG;
     for (int i = 0; i < nphases; ++i) phase_ms[i] = c->phase[i];
     if (sent_bytes) *sent_bytes = c->sent;
+    return LABSORT_OK;
+}
+
+int labsort_dist_collectives(labsort_comm_t c, double *arrive, double *leave, int ncoll) {
+    if (!c || !arrive || !leave || ncoll < 0 || ncoll > dist::C_NCOLL) return LABSORT_ERR_ARG;
+    for (int k = 0; k < ncoll; ++k) {
+        arrive[k] = c->res.arrive[k];
+        leave[k] = c->res.leave[k];
+    }
     return LABSORT_OK;
 }
 

@@ -289,11 +289,12 @@ def make_comm(ls, backend: str = "nccl", group=None):
     return ls.DistComm.rccl(world, rank, obj[0])
 
 
-def dist_sort_splitters(local: torch.Tensor, comm, key: str = "u32", stream=None):
+def dist_sort_splitters(local: torch.Tensor, comm, key: str = "u32", stream=None, copy: bool = True):
     """Sort the global array whose rank-r shard is `local` (device tensor, left
     untouched) with the product's splitter exchange: labsort_dist_sort, the C++ schedule
     of csrc/dist_plan.h (local radix sort, (key, rank, position) splitters from a regular
     sample, pairwise send/recv with every peer at once, merge of the received runs in
-    rank order).  Returns (this rank's contiguous range of the sorted array as a tensor
-    viewing the communicator's buffer, its global offset)."""
-    return comm.sort_tensor(local, local.numel(), key=key, stream=stream)
+    rank order).  Returns (this rank's contiguous range of the sorted array, its global
+    offset); copy=False: the range as a view of the communicator's buffer (kept alive by
+    the view, overwritten by the communicator's next sort)."""
+    return comm.sort_tensor(local, local.numel(), key=key, stream=stream, copy=copy)

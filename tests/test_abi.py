@@ -100,16 +100,6 @@ def test_sizes_and_limits(ls):
     assert ls.workspace_bytes(1 << 20, "radix") >= 8 * (1 << 20)
 
 
-def test_small_radix_workspace(ls, monkeypatch):
-    """LABSORT_RADIX_IMPL=small: one key buffer and a 1 KB histogram row per 16384-key tile"""
-    monkeypatch.setenv("LABSORT_RADIX_IMPL", "small")
-    for n in (ls.tile_keys() + 1, 1 << 20, 1 << 22):
-        w = ls.workspace_bytes(n, "radix")
-        assert 4 * n + ((n + 16383) // 16384) * 1024 <= w < 4 * n + (1 << 20)
-        assert ls.radix_impl(n) == "small"
-    assert ls.radix_impl((1 << 22) + 1) == "gather"
-
-
 def test_argument_errors(ls):
     L = ls.lib
     ws = ctypes.create_string_buffer(1 << 16)

@@ -182,6 +182,70 @@ def test_dist_sort_gloo_world8(oracle):
     _check_world(oracle, 8, [0, 6, 11, 12, 13, 15])
 
 
+# ---- a failing rank ends every rank (labsort_dist_sort's failure agreement) ----------
+FAIL_CASES = [("local_sort", 1), ("bounds", 0), ("recv", -1)]  # -1: the last rank
+
+
+def _fail_worker(rank, world, port, q):
+    """one rank: each failure case in turn (LABSORT_TEST_FAIL=<phase>:<rank>), then a
+    normal sort on the same gloo group -- which only works if every rank left the failed
+    sorts after the same collective"""
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import time
+
+        import oracle as O
+        D = importlib.import_module(PKG_NAME + ".dist")
+        shard = O.gen(3000, 0x5EED0011, "u32", first=rank * 3000)
+        for ci, (phase, fr) in enumerate(FAIL_CASES):
+            os.environ["LABSORT_TEST_FAIL"] = f"{phase}:{fr % world}"
+            t0 = time.monotonic()
+            try:
+                O.dist_sort(shard, "u32", world, rank, D.GlooColl(), cap=3000 * world + 1)
+                status = 0
+            except RuntimeError as e:
+                status = int(str(e).rsplit(" ", 1)[1])
+            q.put((ci, rank, status, time.monotonic() - t0))
+        os.environ.pop("LABSORT_TEST_FAIL")
+        out, goff = O.dist_sort(shard, "u32", world, rank, D.GlooColl(), cap=3000 * world + 1)
+        q.put((len(FAIL_CASES), rank, 0, (out, goff)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_dist_sort_failure_ends_every_rank(oracle, world):
+    """A rank whose local sort, bound queries or receive buffer fails reports its status in
+    the next collective: it returns its own error (LABSORT_ERR_DEVICE, 3) and every other
+    rank LABSORT_ERR_PEER (4), within seconds, instead of waiting for it; the group then
+    sorts normally (the ranks left after the same collective)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world * (len(FAIL_CASES) + 1)):
+        ci, r, st, extra = q.get(timeout=120)
+        got[(ci, r)] = (st, extra)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for ci, (phase, fr) in enumerate(FAIL_CASES):
+        for r in range(world):
+            st, secs = got[(ci, r)]
+            assert st == (3 if r == fr % world else 4), (phase, fr, r, st)
+            assert secs < 30, (phase, r, secs)
+    full = oracle.sort_u32(np.concatenate([oracle.gen(3000, 0x5EED0011, "u32", first=r * 3000) for r in range(world)]))
+    parts = [got[(len(FAIL_CASES), r)][1] for r in range(world)]
+    assert [g for _, g in parts] == list(np.cumsum([0] + [o.size for o, _ in parts])[:-1])
+    np.testing.assert_array_equal(np.concatenate([o for o, _ in parts]), full)
+
+
 def test_schedule_shape():
     D = importlib.import_module(PKG_NAME + ".dist")
     assert len(D.schedule(8)) == 6 and len(D.schedule(2)) == 1 and D.schedule(1) == []

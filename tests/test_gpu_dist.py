@@ -153,3 +153,92 @@ def test_dist_sort_rccl_one_rank(ls, oracle, torch_gpu):
             np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), exp)
     finally:
         comm.close()
+
+
+# ---- a failing rank ends every rank (the status words of dist_plan.h's collectives) ----
+FAIL_CASES = [("local_sort", 1), ("bounds", 0), ("recv", -1)]
+
+
+def _fail_worker(rank, world, port, q):
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import time
+
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ls = importlib.import_module(PKG_NAME)
+        D = importlib.import_module(PKG_NAME + ".dist")
+        comm = D.make_comm(ls, backend="gloo")
+        m = 200_000
+        t = torch.empty(m, dtype=torch.int32, device="cuda")
+        ls.fill(t, m, 0x5EED0012, "u32", first=rank * m)
+        for ci, (phase, fr) in enumerate(FAIL_CASES):
+            os.environ["LABSORT_TEST_FAIL"] = f"{phase}:{fr % world}"
+            t0 = time.monotonic()
+            try:
+                comm.sort(t, m)
+                st = 0
+            except ls.LabsortError as e:
+                st = e.status
+            q.put((ci, rank, st, time.monotonic() - t0))
+        os.environ.pop("LABSORT_TEST_FAIL")
+        out, goff = D.dist_sort_splitters(t, comm)  # the communicator still works
+        torch.cuda.synchronize()
+        q.put((len(FAIL_CASES), rank, 0, (out.cpu().numpy().copy(), goff)))
+        comm.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_sort_failure_ends_every_rank(oracle, world):
+    """labsort_dist_sort with one rank's local sort, bound queries or receive buffer
+    failing (LABSORT_TEST_FAIL): that rank returns LABSORT_ERR_DEVICE, every other rank
+    LABSORT_ERR_PEER, each within seconds, and the next sort on the same communicators
+    succeeds."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world * (len(FAIL_CASES) + 1)):
+        ci, r, st, extra = q.get(timeout=300)
+        got[(ci, r)] = (st, extra)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for ci, (phase, fr) in enumerate(FAIL_CASES):
+        for r in range(world):
+            st, secs = got[(ci, r)]
+            assert st == (3 if r == fr % world else 4), (phase, r, st)
+            assert secs < 30, (phase, r, secs)
+    m = 200_000
+    exp = oracle.sort_u32(oracle.gen(m * world, 0x5EED0012, "u32"))
+    np.testing.assert_array_equal(np.concatenate([got[(len(FAIL_CASES), r)][1][0] for r in range(world)]).view(np.uint32),
+                                  exp)
+
+
+def test_bench_dist_gloo_config5():
+    """bench.py's N > 1 line rehearsed with 2 ranks on one GPU over gloo: BASELINE config 5
+    (2^30 keys partitioned over the ranks: 2^29 each, strong scaling), verified."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+                        os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--steps", "1",
+                        "--warmup", "0", "--no-weak", "--no-host-path"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert "BASELINE config 5" in line["config"]["workload"]
+    assert line["config"]["n_total"] == 1 << 30 and line["config"]["n_per_gpu"] == 1 << 29
+    ph = line["xgmi"]["phases_ms_last_step"]
+    assert ph["plan_work"] >= 0 and ph["plan_wait"] >= 0
+    assert set(line["xgmi"]["collectives_ms_last_step"]) >= {"samples", "counts"}

@@ -106,47 +106,35 @@ def test_gather_default_window(ls):
 
 # ---- the fused small path (gsweep.hip, at most 128 tiles = 2^20 keys): no scan launches;
 # each pass derives its tile's runs from the previous pass's rows and accumulated digit
-# totals.  LABSORT_GS_FUSED: 2 = the default (no memset; pass 1 reads pass 0's rows),
-# 1 = the memset variant, 0 = the scan launches of the larger sizes
-FUSED = ["2", "1", "0"]
-
-
-@pytest.mark.parametrize("fused", FUSED)
+# totals (no memset: pass 1 reads pass 0's rows)
 @pytest.mark.parametrize("mask", [0xFFFF00FF, 0x0F0F0F0F, 0xFF0000FF, 0x000000FF, 0x80000001, 0xFF000000, 0x00FFFF00])
-def test_gather_fused_pass_structure(ls, oracle, torch_gpu, monkeypatch, fused, mask):
+def test_gather_fused_pass_structure(ls, oracle, torch_gpu, monkeypatch, mask):
     """skipped passes forward the digit totals they received (acc[p] <- acc[p - 1])"""
-    monkeypatch.setenv("LABSORT_GS_FUSED", fused)
     n = (1 << 20) - 333
     a = oracle.gen(n, SEED + 31, "u32") & np.uint32(mask)
     for key in ("u32", "i32"):
         np.testing.assert_array_equal(sort_impl(ls, torch_gpu, a, key, "gather", monkeypatch), ref(oracle, a, key))
 
 
-@pytest.mark.parametrize("fused", FUSED)
 @pytest.mark.parametrize("dist", ["u31", "mod100", "mod1000", "const", "sorted", "reversed", "lowbits"])
 @pytest.mark.parametrize("n", [GT + 3, 1 << 20])
-def test_gather_fused_distributions(ls, oracle, torch_gpu, monkeypatch, fused, dist, n):
-    monkeypatch.setenv("LABSORT_GS_FUSED", fused)
+def test_gather_fused_distributions(ls, oracle, torch_gpu, monkeypatch, dist, n):
     a = oracle.gen(n, SEED + 33, dist, param=12 if dist == "lowbits" else 0)
     np.testing.assert_array_equal(sort_impl(ls, torch_gpu, a, "u32", "gather", monkeypatch, inplace=(n & 1) == 1),
                                   oracle.sort_u32(a))
 
 
-@pytest.mark.parametrize("fused", FUSED)
 @pytest.mark.parametrize("case", ["mostly_zero", "two_values", "even_digits", "rare"])
-def test_gather_fused_sparse_digits(ls, oracle, torch_gpu, monkeypatch, fused, case):
+def test_gather_fused_sparse_digits(ls, oracle, torch_gpu, monkeypatch, case):
     """tiles that meet many digits (more than one chunk of runs in the prologue)"""
-    monkeypatch.setenv("LABSORT_GS_FUSED", fused)
     a = _sparse_cases(oracle, (1 << 20) - 5)[case]
     for key in ("u32", "i32"):
         np.testing.assert_array_equal(sort_impl(ls, torch_gpu, a, key, "gather", monkeypatch), ref(oracle, a, key))
 
 
-@pytest.mark.parametrize("fused", FUSED)
-def test_gather_fused_repeat_same_workspace(ls, oracle, torch_gpu, monkeypatch, fused):
+def test_gather_fused_repeat_same_workspace(ls, oracle, torch_gpu, monkeypatch):
     """back-to-back sorts on one workspace: the accumulators a sort leaves behind (and
     garbage before the first) never leak into the next sort"""
-    monkeypatch.setenv("LABSORT_GS_FUSED", fused)
     monkeypatch.setenv("LABSORT_RADIX_IMPL", "gather")
     n = 500_000
     ws = torch_gpu.full((max(ls.workspace_bytes(n, "radix"), 256),), 0xA5, dtype=torch_gpu.uint8, device="cuda")
@@ -159,12 +147,10 @@ def test_gather_fused_repeat_same_workspace(ls, oracle, torch_gpu, monkeypatch, 
         np.testing.assert_array_equal(from_dev(o), oracle.sort_u32(a))
 
 
-@pytest.mark.parametrize("plan_zero", ["1", "0"])
 @pytest.mark.parametrize("inplace", [False, True])
-def test_onesweep_lookback_clear(ls, oracle, torch_gpu, monkeypatch, plan_zero, inplace):
-    """the look-back clear folded into the plan launch (default) or as its own k_zero
-    (LABSORT_PLAN_ZERO=0); a dirty workspace from the previous sort must not leak"""
-    monkeypatch.setenv("LABSORT_PLAN_ZERO", plan_zero)
+def test_onesweep_lookback_clear(ls, oracle, torch_gpu, monkeypatch, inplace):
+    """the look-back clear folded into a launch; a dirty workspace from the previous sort
+    must not leak"""
     n = (1 << 22) + 4097
     for i in range(2):
         a = oracle.gen(n, SEED + 50 + i, "u32")

@@ -26,6 +26,12 @@ def test_sort_host_ranks_peer(ls, oracle, torch_gpu, p, dist, key, n):
     np.testing.assert_array_equal(b.view(np.uint32), exp)
     t, sent = ls.multi_timing()
     assert t["total"] > 0 and sent <= n * 4
+    # the plan's work and wait (time inside its collectives), every rank's arrival times
+    assert t["plan_work"] >= 0 and t["plan_wait"] >= 0
+    for c in ls.multi_collectives(p):
+        for k in ("samples", "counts"):
+            assert 0 <= c[k][0] <= c[k][1]
+        assert c["samples"][1] <= c["counts"][0]
 
 
 def test_sort_host_ranks_balance_const(ls, oracle, torch_gpu):
@@ -52,6 +58,21 @@ def test_sort_host_ranks_rccl_one_rank(ls, oracle, torch_gpu):
     a = oracle.gen(n, 0x5EED7400, "u32")
     b = a.copy()
     ls.sort_host_ranks(b, [0], transport="rccl")
+    np.testing.assert_array_equal(b, oracle.sort_u32(a))
+
+
+@pytest.mark.parametrize("phase", ["local_sort", "bounds", "recv"])
+def test_sort_host_ranks_rank_failure(ls, oracle, torch_gpu, monkeypatch, phase):
+    """one in-process rank failing (LABSORT_TEST_FAIL) ends the call with that rank's own
+    error (LABSORT_ERR_DEVICE), not a hang; the next call works"""
+    monkeypatch.setenv("LABSORT_TEST_FAIL", f"{phase}:2")
+    a = oracle.gen(300_000, 0x5EED7500, "u32")
+    with pytest.raises(ls.LabsortError) as e:
+        ls.sort_host_ranks(a.copy(), [0] * 4, transport="peer")
+    assert e.value.status == ls.ERR_DEVICE
+    monkeypatch.delenv("LABSORT_TEST_FAIL")
+    b = a.copy()
+    ls.sort_host_ranks(b, [0] * 4, transport="peer")
     np.testing.assert_array_equal(b, oracle.sort_u32(a))
 
 

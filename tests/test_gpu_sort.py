@@ -318,6 +318,19 @@ def test_sort_host_algorithms(ls, oracle, torch_gpu, algo):
     np.testing.assert_array_equal(b, oracle.sort_u32(a))
 
 
+@pytest.mark.parametrize("n,off", [(1, 0), (4095, 0), (16384 * 3 + 5, 0), ((1 << 22) + 7, 0), (100_001, 1)])
+def test_copy(ls, oracle, torch_gpu, n, off):
+    """labsort_copy (the bench's copy ceiling): 16-B tiles, word tail, unaligned views"""
+    torch = torch_gpu
+    a = oracle.gen(n + off, SEED + 77, "u32")
+    t = to_dev(torch, a)
+    o = torch.zeros(n + 2, dtype=torch.int32, device="cuda")
+    ls.copy(t[off:], o[1 if off else 0:], n)
+    torch.cuda.synchronize()
+    got = from_dev(o)
+    np.testing.assert_array_equal(got[(1 if off else 0):(1 if off else 0) + n], a[off:])
+
+
 def test_count_descents(ls, oracle, torch_gpu):
     torch = torch_gpu
     a = np.arange(10_000, dtype=np.uint32)
@@ -329,7 +342,7 @@ def test_count_descents(ls, oracle, torch_gpu):
     assert int(c.item()) == 3
 
 
-@pytest.mark.parametrize("impl", ["gather", "onesweep", "small"])
+@pytest.mark.parametrize("impl", ["gather", "onesweep"])
 def test_timing_hooks(ls, oracle, torch_gpu, monkeypatch, impl):
     torch = torch_gpu
     monkeypatch.setenv("LABSORT_RADIX_IMPL", impl)
@@ -340,11 +353,11 @@ def test_timing_hooks(ls, oracle, torch_gpu, monkeypatch, impl):
     ls.timing_enable(True)
     ls.sort_device(t, o, n, algo="radix")
     torch.cuda.synchronize()
-    ms, cnt = ls.timing_read({"gather": "gsweep", "onesweep": "onesweep", "small": "small"}[impl])
+    ms, cnt = ls.timing_read({"gather": "gsweep", "onesweep": "onesweep"}[impl])
     ms2, cnt2 = ls.timing_read("gcopy")
     ls.timing_enable(False)
-    # four 8-bit passes (gather: pass 0 always runs, 1-3 active here); small: one launch
-    assert cnt == (1 if impl == "small" else 4) and ms > 0
+    # four 8-bit passes (gather: pass 0 always runs, 1-3 active here)
+    assert cnt == 4 and ms > 0
     assert cnt2 == (1 if impl == "gather" else 0)
 
 
@@ -370,43 +383,6 @@ def test_sort_device_pass_structure(ls, oracle, torch_gpu, monkeypatch, mask, na
     ls.sort_device(t, o, n, key=key, algo="radix")
     torch.cuda.synchronize()
     np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key), err_msg=name)
-
-
-# ---- single-launch radix (small.hip, LABSORT_RADIX_IMPL=small) ------------------------
-@pytest.mark.parametrize("mask", [0xFFFFFFFF, 0xFFFF00FF, 0x000000FF, 0x80000001, 0x0])
-@pytest.mark.parametrize("key", ["u32", "i32"])
-@pytest.mark.parametrize("n", [32768 + 1, 100_003, 1 << 20, (1 << 22)])
-@pytest.mark.parametrize("inplace", [False, True])
-def test_small_radix(ls, oracle, torch_gpu, monkeypatch, mask, key, n, inplace):
-    """All active-pass counts 0-4 (mask), odd counts in place (the final copy), partial
-    last tiles and the 256-tile maximum, against std::sort; the error word stays 0."""
-    torch = torch_gpu
-    monkeypatch.setenv("LABSORT_RADIX_IMPL", "small")
-    assert ls.radix_impl(n) == "small"
-    a = oracle.gen(n, SEED + 40 + n, "u32") & np.uint32(mask)
-    t = to_dev(torch, a)
-    o = t if inplace else torch.empty_like(t)
-    ws = torch.empty(ls.workspace_bytes(n, "radix"), dtype=torch.uint8, device="cuda")
-    ws.fill_(0xA5)  # stale barrier word and error word from an earlier user
-    for _ in range(2):  # a second sort on the same workspace re-tags the barrier
-        if inplace:
-            t.copy_(to_dev(torch, a))
-        ls.sort_device(t, o, n, key=key, algo="radix", workspace=ws)
-        ls.workspace_status(ws, n, "radix")
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key))
-
-
-@pytest.mark.parametrize("dist", ["sorted", "reversed", "mod1000", "const", "lowbits"])
-def test_small_radix_distributions(ls, oracle, torch_gpu, monkeypatch, dist):
-    torch = torch_gpu
-    monkeypatch.setenv("LABSORT_RADIX_IMPL", "small")
-    n = (1 << 20) + 3
-    a = oracle.gen(n, SEED + 41, dist, param=9)
-    t = to_dev(torch, a)
-    ls.sort_device(t, t, n, algo="radix")
-    torch.cuda.synchronize()
-    np.testing.assert_array_equal(from_dev(t), oracle.sort_u32(a))
 
 
 OSP_TILE = 16384   # k_onesweep_p tile (csrc/common.h OSP_TILE)
