@@ -1,5 +1,5 @@
 // lsweep_probe.hip -- times the local first pass (csrc/lsweep.hip, k_lsweep) at 2^28 keys
-// against a tiled 16-B copy of the same bytes, with and without the joint-field counting,
+// against a tiled 16-B copy of the same bytes (joint-field counting included),
 // for uniform / sorted / %100 / %1000 keys, and checks a few tiles on the host.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o lsweep_probe lsweep_probe.hip
 #include "../../radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd/csrc/lsweep.hip"
@@ -96,21 +96,19 @@ int main(int argc, char **argv) {
     for (int dist = 0; dist < 4; ++dist) {
         k_fillp<<<8192, 256>>>(in, n, dist);
         CK(hipDeviceSynchronize());
-        for (int joint_on : {0, 2, 5, 6}) {
-            for (int grid : {cus}) {
-                float t = timeit([&] {
-                    (void)hipMemsetAsync(tot0, 0, 1024, 0);
-                    (void)hipMemsetAsync(joint, 0, 4 * NSEG * 256 * 4, 0);
-                    (void)launch_lsweep(in, out, n, 0u, rows, tot0, joint, grid, joint_on, 0);
-                });
-                printf("lsweep %-8s joint=%d grid=%4d %.4f ms  %7.1f GB/s\n", dn[dist], joint_on, grid, t, gb / t * 1e3);
-            }
+        {
+            float t = timeit([&] {
+                (void)hipMemsetAsync(tot0, 0, 1024, 0);
+                (void)hipMemsetAsync(joint, 0, 4 * NSEG * 256 * 4, 0);
+                (void)launch_lsweep(in, out, n, 0u, rows, tot0, joint, 0);
+            });
+            printf("lsweep %-8s %.4f ms  %7.1f GB/s\n", dn[dist], t, gb / t * 1e3);
         }
         // host check: every tile sorted by digit 0 (stably) and the counts
         std::vector<uint32_t> hi(n), ho(n), hr((size_t)ntiles * 256), ht(256), hj(4 * NSEG * 256);
         CK(hipMemset(tot0, 0, 1024));
         CK(hipMemset(joint, 0, 4 * NSEG * 256 * 4));
-        CK(launch_lsweep(in, out, n, 0u, rows, tot0, joint, cus, 5, 0));
+        CK(launch_lsweep(in, out, n, 0u, rows, tot0, joint, 0));
         CK(hipDeviceSynchronize());
         CK(hipMemcpy(hi.data(), in, n * 4, hipMemcpyDeviceToHost));
         CK(hipMemcpy(ho.data(), out, n * 4, hipMemcpyDeviceToHost));

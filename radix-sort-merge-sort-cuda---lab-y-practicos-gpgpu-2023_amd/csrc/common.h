@@ -38,7 +38,8 @@ static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass til
 // ---- local first pass (lsweep.hip): tiles sorted by digit 0 in place, rows of counts ----
 constexpr int LS_BLOCK = 1024, LS_KPT = 16, LS_TILE = LS_BLOCK * LS_KPT;
 hipError_t launch_lsweep(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, uint32_t *rows, uint32_t *tot0,
-                         uint32_t *joint, int grid, int mode, hipStream_t s);
+                         uint32_t *joint, hipStream_t s);
+constexpr int LS_GROUP = 64;  // tiles per k_lscan workgroup
 
 // ---- segmented look-back chains (8-bit radix) ----
 // Each pass's input is split into NSEG contiguous segments, each with its own

@@ -1332,6 +1332,40 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
     }
 }
 
+// k_lcopy: no active digit after digit 0 (the local pass's logical order is the sorted
+// array): workgroup k gathers logical tile k from TMP into OUT.  Every other sort exits.
+__global__ __launch_bounds__(OSP_BLOCK) void k_lcopy(Bufs b, const Plan *__restrict__ plan, GthTables tb, uint32_t n) {
+    if (plan->copy_from != SEL_TMP) return;
+    __shared__ GthS G;
+    constexpr int KPT = OSP_KPT;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t L0 = blockIdx.x * (uint32_t)OSP_TILE, nv = n - L0 < (uint32_t)OSP_TILE ? n - L0 : (uint32_t)OSP_TILE;
+    uint32_t e0, e1, a, bb, s;
+    gth_range(tb, L0, e0, e1);
+    gth_run(tb, e0, e1, tid, a, bb, s);
+    if (tid < (uint32_t)(OSP_TILE / 64)) G.mask[tid] = 0ull;
+    if (tid == 0) {
+        G.over = e1 - e0 >= (uint32_t)GTH_KMAX;
+        G.e0 = e0;
+        G.e1 = e1;
+    }
+    __syncthreads();
+    gth_mark(G, a, bb, L0, nv);
+    __syncthreads();
+    if (wid == 0) gth_prefix(G, lane);
+    __syncthreads();
+    gth_delta(G, a, bb, s, L0, nv);
+    __syncthreads();
+    uint32_t k[KPT];
+    gth_load<KPT>(G, tb, osp_rsrc(b.p[SEL_TMP], n), L0, nv, wid, lane, 0u, 0, k);
+    const __amdgpu_buffer_rsrc_t rout = osp_rsrc(b.p[SEL_OUT], n);
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+        const uint32_t p = (wid * KPT + (uint32_t)j) * 64u + lane;
+        if (p < nv) __builtin_amdgcn_raw_buffer_store_b32(k[j], rout, (L0 + p) * 4u, 0, 0);
+    }
+}
+
 // ---------------------------------------------------------------------------------
 // LDS-resident tile sort: 8-bit LSD passes entirely in LDS, one global read and write
 // ---------------------------------------------------------------------------------
@@ -1493,6 +1527,160 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
             const uint32_t idx = wbase + j * WAVE;
             if (idx < n) vout[idx] = v[j];
         }
+    }
+}
+
+// Keys-only tile sort, persistent and pipelined (merge sort stage 1, the tile-sort small
+// path).  The non-persistent k_tile_sort above holds one 32768-key tile per CU (146 KB of
+// LDS): a workgroup's load waits for nothing else to do, and its four LDS passes leave
+// the memory idle.  Here one 512-thread workgroup per CU (8 wave64s, 64 keys per lane,
+// two waves per SIMD: room for 256 VGPRs) loops over the tiles, the next tile's keys
+// loading into registers while the current one is ranked and reordered in LDS, so each
+// CU's HBM traffic overlaps its LDS work.  Same passes, ranks and uniform-digit skip.
+constexpr int TSP_BLOCK = 512, TSP_KPT = 64;
+static_assert(TSP_BLOCK * TSP_KPT == TS_TILE, "one tile per workgroup iteration");
+struct TspSmem {
+    uint32_t keys[TS_TILE];
+    uint32_t whist[(TSP_BLOCK / WAVE) * 256];
+    uint32_t wsum[8];
+    uint32_t red_and[TSP_BLOCK / WAVE];
+    uint32_t red_or[TSP_BLOCK / WAVE];
+    uint32_t probe[WAVE];
+    uint32_t ordered;
+};
+__global__ __launch_bounds__(TSP_BLOCK, 2) void k_tile_sort_p(const uint32_t *in, uint32_t *out, uint32_t n,
+                                                             uint32_t flip) {
+    constexpr int KPT = TSP_KPT, W = TSP_BLOCK / WAVE, R = 256, TILE = TS_TILE;
+    __shared__ TspSmem sm;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+    const uint32_t sentinel = ~flip;
+    const uint32_t ntiles = (n + (uint32_t)TILE - 1u) / (uint32_t)TILE;
+    if (wid == 0) {  // lane-ordered LDS atomics (see k_onesweep_p): rank by one atomic per key
+        const bool ord = lds_lane_ordered(sm.probe, lane);
+        if (lane == 0) sm.ordered = ord ? 1u : 0u;
+    }
+    const __amdgpu_buffer_rsrc_t rin = osp_rsrc(in, n), rout = osp_rsrc(out, n);
+    const uint32_t woff = wid * (KPT * WAVE) + lane;
+    // slot j of a lane at byte offset o + j * 256: as 4 base offsets (one per 16 slots) and
+    // immediate offsets below 4 KiB, so no slot needs an address register of its own
+    auto load = [&](uint32_t t, uint32_t (&k)[KPT]) {  // past n: the sentinel (digit 255)
+        const uint32_t o = (t * (uint32_t)TILE + woff) * 4u;
+        const uint32_t nv = n - t * (uint32_t)TILE;
+#pragma unroll
+        for (int q = 0; q < KPT / 16; ++q) {
+            const uint32_t oq = o + (uint32_t)q * 16u * WAVE * 4u;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int j = q * 16 + i;
+                const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rin, oq, i * WAVE * 4, 0);
+                k[j] = woff + j * WAVE < nv ? v : sentinel;
+            }
+        }
+    };
+    uint32_t k[KPT], kn[KPT];
+    uint32_t t = blockIdx.x;
+    if (t < ntiles) load(t, kn);
+    __syncthreads();
+    const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
+    uint32_t *wh = sm.whist + wid * R;
+    for (; t < ntiles; t += gridDim.x) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) k[j] = kn[j];
+        if (t + gridDim.x < ntiles) load(t + gridDim.x, kn);
+        const uint32_t nv = n - t * (uint32_t)TILE;
+        // bits on which the tile's keys differ -> passes that are not the identity
+        uint32_t a = ~0u, o = 0u;
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const bool ok = woff + j * WAVE < nv;
+            const uint32_t x = k[j] ^ flip;
+            a &= ok ? x : ~0u;
+            o |= ok ? x : 0u;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            a &= __shfl_xor(a, off);
+            o |= __shfl_xor(o, off);
+        }
+        if (lane == 0) {
+            sm.red_and[wid] = a;
+            sm.red_or[wid] = o;
+        }
+        __syncthreads();
+        uint32_t diff;
+        {
+            uint32_t aa = ~0u, oo = 0u;
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+                aa &= sm.red_and[w];
+                oo |= sm.red_or[w];
+            }
+            diff = aa ^ oo;
+        }
+        for (int pass = 0; pass < 4; ++pass) {
+            const uint32_t shift = pass * 8;
+            if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the tile
+            for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
+            uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                // (16 returning atomics in flight at most: the scheduler would otherwise
+                // hoist all 64 and their results and addresses out of the 256 VGPRs)
+                if (j % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+                const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+                uint32_t r;
+                if (atomic_rank) {
+                    r = wave_atomic_rank(wh, d, lane);
+                } else {
+                    const uint64_t m = match8(d);
+                    const uint32_t pre = mbcnt64(m);
+                    const uint32_t old = wh[d];
+                    if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
+                    r = old + pre;
+                }
+                rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
+            }
+            __syncthreads();
+            uint32_t tot = 0;
+            if (tid < (uint32_t)R) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) tot += sm.whist[w * R + tid];
+            }
+            const uint32_t ds = block_excl_scan<TSP_BLOCK, R>(tot, sm.wsum);
+            if (tid < (uint32_t)R) {
+                uint32_t run = ds;
+#pragma unroll
+                for (int w = 0; w < W; ++w) {
+                    const uint32_t c = sm.whist[w * R + tid];
+                    sm.whist[w * R + tid] = run;
+                    run += c;
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                if (j % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+                const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+                sm.keys[wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = k[j];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                if (j % 16 == 0) __builtin_amdgcn_sched_barrier(0);
+                k[j] = sm.keys[woff + j * WAVE];
+            }
+        }
+        const uint32_t o4 = (t * (uint32_t)TILE + woff) * 4u;
+#pragma unroll
+        for (int q = 0; q < KPT / 16; ++q) {
+            const uint32_t oq = o4 + (uint32_t)q * 16u * WAVE * 4u;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int j = q * 16 + i;
+                if (woff + j * WAVE < nv) __builtin_amdgcn_raw_buffer_store_b32(k[j], rout, oq, i * WAVE * 4, 0);
+            }
+        }
+        __syncthreads();  // every wave has read this tile (LDS keys, red_*) before the next one's writes
     }
 }
 
@@ -1922,6 +2110,26 @@ hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint3
     return hipGetLastError();
 }
 
+hipError_t launch_plan_l(const uint32_t *tot0, const uint32_t *joint, size_t n, Plan *plan, SegPlan *segplans,
+                         uint32_t *hist, void *zero_p, size_t zero_bytes, hipStream_t s) {
+    // the look-back clear rides in the plan launch (workgroups 1..)
+    const bool fold = zero_bytes % 16 == 0;
+    if (!fold && zero_bytes) {
+        const hipError_t z = launch_zero(zero_p, zero_bytes, s);
+        if (z != hipSuccess) return z;
+    }
+    const size_t zn4 = fold ? zero_bytes / 16 : 0;
+    const unsigned g = 1u + (zn4 ? blocks_for(zn4, 256 * 4, 2048) : 0u);
+    k_plan_l<<<g, 256, 0, s>>>(tot0, joint, (uint32_t)n, plan, segplans, hist, static_cast<uint4 *>(zero_p), zn4);
+    return hipGetLastError();
+}
+
+hipError_t launch_lcopy(Bufs b, const Plan *plan, GthTables tb, size_t n, hipStream_t s) {
+    const unsigned g = (unsigned)((n + OSP_TILE - 1) / OSP_TILE);
+    k_lcopy<<<g, OSP_BLOCK, 0, s>>>(b, plan, tb, (uint32_t)n);
+    return hipGetLastError();
+}
+
 hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, uint32_t *joint,
                            hipStream_t s) {
     if (n == 0) return hipSuccess;
@@ -1977,7 +2185,11 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) 
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t nt = (n + TS_TILE - 1) / TS_TILE;
-    k_tile_sort<TS_BLOCK, TS_KPT><<<(unsigned)nt, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
+    const char *e = std::getenv("LABSORT_TS_IMPL");  // (r4 A/B, removed after)
+    if (e && e[0] == 'p')
+        k_tile_sort_p<<<(unsigned)(nt < (size_t)cu_count() ? nt : (size_t)cu_count()), TSP_BLOCK, 0, s>>>(in, out, (uint32_t)n, flip);
+    else
+        k_tile_sort<TS_BLOCK, TS_KPT><<<(unsigned)nt, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
     return hipGetLastError();
 }
 

@@ -56,52 +56,23 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t ls_rsrc(const uint32_t *p, uin
     return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), (short)0, (int)(n * 4u), 0x00020000);
 }
 
-// The three joint fields of 4 consecutive sorted slots (keys already ^ flip) counted into
-// jh: a field the 4 keys share is added once (+4), and once per wave (+256) when every
-// lane's 4 keys share the same value (sorted or low-entropy keys), instead of by many
-// lanes serialised on one LDS counter.  All 64 lanes active.
-__device__ __forceinline__ void ls_count4(uint32_t *jh, const uint32_t (&x)[4], uint32_t lane) {
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-        const uint32_t sh = 8u * p + 4u;
-        const uint32_t f0 = (x[0] >> sh) & (LJF - 1u);
-        const bool same = ((x[1] >> sh) & (LJF - 1u)) == f0 && ((x[2] >> sh) & (LJF - 1u)) == f0 &&
-                          ((x[3] >> sh) & (LJF - 1u)) == f0;
-        const uint32_t w0 = __builtin_amdgcn_readfirstlane(f0);
-        if (__ballot(!(same && f0 == w0)) == 0ull) {
-            if (lane == 0) atomicAdd(jh + p * LJF + w0, 4u * WAVE);
-        } else if (same) {
-            atomicAdd(jh + p * LJF + f0, 4u);
-        } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) atomicAdd(jh + p * LJF + ((x[q] >> sh) & (LJF - 1u)), 1u);
-        }
-    }
+// Joint fields of one key slot of a wave, counted into jh (3 x 4096 counters): fields
+// f_p = (key ^ flip) >> (8p + 4), 12 bits (the top nibble of digit p and digit p + 1).
+// Random keys: one LDS add per lane and field.  A wave whose keys repeat a field (sorted,
+// clustered or small keys: many lanes on one counter would serialise) adds each run of
+// equal values in consecutive lanes once instead: lane-run leaders by one shuffle and
+// one ballot, the run length from the next leader.  The choice is made per wave and
+// tile from its first slot (another lane sharing lane 0's value: 1 in 64 for uniform
+// 12-bit fields).  ok: the lane holds a real key (partial last tile).
+__device__ __forceinline__ void ls_count_runs(uint32_t *jh, uint32_t f, bool ok, uint32_t lane) {
+    const uint32_t fp = __shfl_up(f, 1);
+    const bool lead = ok && (lane == 0 || f != fp);
+    const uint64_t L = __ballot(lead);
+    const uint64_t after = L & ~((2ull << lane) - 1ull);  // leaders after this lane (lane 63: none)
+    const uint32_t next = after ? (uint32_t)__builtin_ctzll(after) : (uint32_t)__popcll(__ballot(ok));
+    if (lead) atomicAdd(jh + f, next - lane);
 }
-
-// Joint-field count of one key slot of a wave (f = the lane's field, ok = the lane holds
-// a real key).  low: the field has few distinct values in this wave (sorted, clustered
-// or small keys): the values are peeled off one at a time (one ballot each) and every
-// distinct value is added once, instead of many lanes serialised on one LDS counter;
-// after 8 values the rest are added lane by lane.  Otherwise one add per lane.
-__device__ __forceinline__ void ls_count_slot(uint32_t *jh, uint32_t f, bool ok, bool low, uint32_t lane) {
-    if (low) {  // (wave-uniform)
-        uint64_t act = __ballot(ok);
-#pragma unroll 1
-        for (int it = 0; act && it < 8; ++it) {
-            const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)f, (int)__builtin_ctzll(act));
-            const uint64_t m = __ballot(f == v) & act;
-            if (lane == (uint32_t)__builtin_ctzll(m)) atomicAdd(jh + v, (uint32_t)__popcll(m));
-            act &= ~m;
-        }
-        if ((act >> lane) & 1ull) atomicAdd(jh + f, 1u);
-    } else if (ok) {
-        atomicAdd(jh + f, 1u);
-    }
-}
-// A field is low-entropy in this wave when another lane of its first slot shares lane
-// 0's value (1 in 4096 for uniform 12-bit fields): decided once per tile and wave.
-__device__ __forceinline__ bool ls_low(uint32_t f) {
+__device__ __forceinline__ bool ls_repeats(uint32_t f) {
     const uint32_t f0 = __builtin_amdgcn_readfirstlane(f);
     return __popcll(__ballot(f == f0)) > 1;
 }
@@ -113,7 +84,6 @@ __device__ __forceinline__ bool ls_low(uint32_t f) {
 // rows[t * 256 + d] = local offset of digit d in tile t | count << 16.  tot0[d] += the
 // digit-0 counts, joint[((p + 1) * NSEG + nibble) * 256 + digit] += the joint fields
 // (both zeroed by the caller).
-template <int JOINT>
 __global__ __launch_bounds__(LB, 4) void k_lsweep(const uint32_t *__restrict__ in, uint32_t *__restrict__ out, uint32_t n,
                                                  uint32_t flip, uint32_t *__restrict__ rows, uint32_t *__restrict__ tot0,
                                                  uint32_t *__restrict__ joint) {
@@ -121,8 +91,7 @@ __global__ __launch_bounds__(LB, 4) void k_lsweep(const uint32_t *__restrict__ i
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
     const uint32_t ntiles = (n + (uint32_t)LT - 1u) / (uint32_t)LT;
     for (uint32_t i = tid; i < (uint32_t)(LW * 256); i += LB) sm.wh[i] = 0u;
-    if constexpr (JOINT != 0)
-        for (uint32_t i = tid; i < (uint32_t)(3 * LJF); i += LB) sm.jh[i] = 0u;
+    for (uint32_t i = tid; i < (uint32_t)(3 * LJF); i += LB) sm.jh[i] = 0u;
     if (wid == 0) {
         const bool ord = lds_lane_ordered(sm.probe, lane);
         if (lane == 0) sm.ordered = ord ? 1u : 0u;
@@ -172,41 +141,26 @@ __global__ __launch_bounds__(LB, 4) void k_lsweep(const uint32_t *__restrict__ i
                 r = old + pre;
             }
             rk[j / 2] = (j & 1) ? rk[j / 2] | (r << 16) : r;
-            if constexpr (JOINT == 6) {
-                const uint32_t x = kB[j] ^ flip;
-                if (woff + j * WAVE < nvalid)
+        }
+        // the joint fields (3 per key), plain adds unless this wave's keys repeat them
+        {
+            bool rep = false;
+#pragma unroll
+            for (int p = 0; p < 3; ++p) rep |= ls_repeats(((kB[0] ^ flip) >> (8 * p + 4)) & (LJF - 1u));
+            if (!rep && nvalid == (uint32_t)LT) {
+#pragma unroll
+                for (int j = 0; j < LK; ++j) {
+                    const uint32_t x = kB[j] ^ flip;
 #pragma unroll
                     for (int p = 0; p < 3; ++p) atomicAdd(sm.jh + p * LJF + ((x >> (8 * p + 4)) & (LJF - 1u)), 1u);
-            }
-        }
-        if constexpr (JOINT == 5) {
-            bool low[3];
+                }
+            } else {
 #pragma unroll
-            for (int p = 0; p < 3; ++p) low[p] = ls_low(((kB[0] ^ flip) >> (8 * p + 4)) & (LJF - 1u));
+                for (int j = 0; j < LK; ++j) {
+                    const uint32_t x = kB[j] ^ flip;
+                    const bool ok = woff + j * WAVE < nvalid;
 #pragma unroll
-            for (int j = 0; j < LK; ++j) {
-                const uint32_t x = kB[j] ^ flip;
-                const bool ok = woff + j * WAVE < nvalid;
-#pragma unroll
-                for (int p = 0; p < 3; ++p) ls_count_slot(sm.jh + p * LJF, (x >> (8 * p + 4)) & (LJF - 1u), ok, low[p], lane);
-            }
-        }
-        if constexpr (JOINT == 2 || JOINT == 4) {
-#pragma unroll
-            for (int j = 0; j < LK; ++j) {
-                const uint32_t x = kB[j] ^ flip;
-                const bool ok = woff + j * WAVE < nvalid;
-#pragma unroll
-                for (int p = 0; p < 3; ++p) {
-                    const uint32_t f = (x >> (8 * p + 4)) & (LJF - 1u);
-                    if (JOINT == 4 && p > 0) {
-                        const uint32_t f0 = __builtin_amdgcn_readfirstlane(f);
-                        if (__ballot(f != f0 || !ok) == 0ull) {
-                            if (lane == 0) atomicAdd(sm.jh + p * LJF + f0, 64u);
-                            continue;
-                        }
-                    }
-                    if (ok) atomicAdd(sm.jh + p * LJF + f, 1u);
+                    for (int p = 0; p < 3; ++p) ls_count_runs(sm.jh + p * LJF, (x >> (8 * p + 4)) & (LJF - 1u), ok, lane);
                 }
             }
         }
@@ -242,35 +196,19 @@ __global__ __launch_bounds__(LB, 4) void k_lsweep(const uint32_t *__restrict__ i
                 const uint32_t q = (uint32_t)g * LB + tid;  // slots 4q .. 4q + 3
                 const uint4 v = *reinterpret_cast<const uint4 *>(sm.keys + ls_pad(4u * q));
                 __builtin_amdgcn_raw_buffer_store_b128(u32x4{v.x, v.y, v.z, v.w}, rout, (beg + 4u * q) * 4u, 0, 0);
-                // the joint fields, counted on the sorted tile (the write-out's registers:
-                // the ranked keys are dead here)
-                if constexpr (JOINT == 1) ls_count4(sm.jh, {v.x ^ flip, v.y ^ flip, v.z ^ flip, v.w ^ flip}, lane);
-                if constexpr (JOINT == 3) {
-                    const uint32_t xs[4] = {v.x ^ flip, v.y ^ flip, v.z ^ flip, v.w ^ flip};
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-#pragma unroll
-                        for (int p = 0; p < 3; ++p) atomicAdd(sm.jh + p * LJF + ((xs[q] >> (8 * p + 4)) & (LJF - 1u)), 1u);
-                }
             }
         } else {
 #pragma unroll
             for (int j = 0; j < LK; ++j) {
                 const uint32_t i = (uint32_t)j * LB + tid;
-                if (i < nvalid) {
-                    const uint32_t v = sm.keys[ls_pad(i)];
-                    __builtin_amdgcn_raw_buffer_store_b32(v, rout, (beg + i) * 4u, 0, 0);
-                    if constexpr (JOINT == 1 || JOINT == 3)
-#pragma unroll
-                        for (int p = 0; p < 3; ++p) atomicAdd(sm.jh + p * LJF + (((v ^ flip) >> (8 * p + 4)) & (LJF - 1u)), 1u);
-                }
+                if (i < nvalid) __builtin_amdgcn_raw_buffer_store_b32(sm.keys[ls_pad(i)], rout, (beg + i) * 4u, 0, 0);
             }
         }
         // each wave clears its own counters (read by no other wave before barrier (1))
         for (uint32_t i = lane; i < 256u; i += WAVE) wh[i] = 0u;
     }
     if (tid < 256u && ctot) atomicAdd(tot0 + tid, ctot);
-    if constexpr (JOINT != 0) {
+    {
         __syncthreads();
         // field f = (digit p+1) << 4 | (top nibble of digit p) -> joint[p+1][nibble][digit];
         // each workgroup starts its flush at a different place, so the atomics of
@@ -297,7 +235,7 @@ __global__ __launch_bounds__(LB, 4) void k_lsweep(const uint32_t *__restrict__ i
 // the error word); 4 threads per digit, 16 tiles each.  The digit-major writes go through
 // LDS so each is a 256-B line segment.
 // ---------------------------------------------------------------------------------
-constexpr int LG = 64;
+constexpr int LG = LS_GROUP;
 __global__ __launch_bounds__(1024) void k_lscan(const uint32_t *__restrict__ rows, const uint32_t *__restrict__ tot0,
                                                 uint32_t *flags, uint32_t *gctr, uint32_t *err, uint32_t *__restrict__ ls,
                                                 uint32_t *__restrict__ sr, uint32_t *__restrict__ first, uint32_t ntp,
@@ -374,19 +312,23 @@ __global__ __launch_bounds__(1024) void k_lscan(const uint32_t *__restrict__ row
 }
 
 hipError_t launch_lsweep(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, uint32_t *rows, uint32_t *tot0,
-                         uint32_t *joint, int grid, int mode, hipStream_t s) {
+                         uint32_t *joint, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t ntiles = (n + LT - 1) / LT;
-    const unsigned g = (unsigned)(ntiles < (size_t)grid ? ntiles : (size_t)grid);
-    switch (mode) {
-    case 0: k_lsweep<0><<<g, LB, 0, s>>>(in, out, (uint32_t)n, flip, rows, tot0, joint); break;
-    case 1: k_lsweep<1><<<g, LB, 0, s>>>(in, out, (uint32_t)n, flip, rows, tot0, joint); break;
-    case 2: k_lsweep<2><<<g, LB, 0, s>>>(in, out, (uint32_t)n, flip, rows, tot0, joint); break;
-    case 3: k_lsweep<3><<<g, LB, 0, s>>>(in, out, (uint32_t)n, flip, rows, tot0, joint); break;
-    case 4: k_lsweep<4><<<g, LB, 0, s>>>(in, out, (uint32_t)n, flip, rows, tot0, joint); break;
-    case 5: k_lsweep<5><<<g, LB, 0, s>>>(in, out, (uint32_t)n, flip, rows, tot0, joint); break;
-    default: k_lsweep<6><<<g, LB, 0, s>>>(in, out, (uint32_t)n, flip, rows, tot0, joint); break;
-    }
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    const unsigned g = (unsigned)(ntiles < (size_t)cus ? ntiles : (size_t)cus);  // one workgroup per CU (LDS-bound)
+    k_lsweep<<<g, LB, 0, s>>>(in, out, (uint32_t)n, flip, rows, tot0, joint);
+    return hipGetLastError();
+}
+
+hipError_t launch_lscan(const uint32_t *rows, const uint32_t *tot0, uint32_t *flags, uint32_t *gctr, uint32_t *err,
+                        GthTables tb, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t ntp = (uint32_t)((n + LT - 1) / LT), ng = (ntp + LG - 1) / LG;
+    k_lscan<<<ng, 1024, 0, s>>>(rows, tot0, flags, gctr, err, const_cast<uint32_t *>(tb.ls), const_cast<uint32_t *>(tb.sr),
+                                const_cast<uint32_t *>(tb.first), ntp, (uint32_t)n);
     return hipGetLastError();
 }
 
