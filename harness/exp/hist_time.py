@@ -12,7 +12,7 @@ d = torch.empty(n, dtype=torch.int32, device="cuda")
 ls.fill(d, n, 0x5EED0003, os.environ.get("DIST", "u32"))
 o = torch.empty_like(d)
 algo = os.environ.get("ALGO", "radix")
-classes = ("histogram", "onesweep") if algo == "radix" else ("tile_sort", "merge")
+classes = ("lsweep", "histogram", "onesweep") if algo == "radix" else ("tile_sort", "merge")
 ws = torch.empty(ls.workspace_bytes(n, algo), dtype=torch.uint8, device="cuda")
 for _ in range(3):
     ls.sort_device(d, o, n, algo=algo, workspace=ws)
@@ -21,7 +21,8 @@ ls.timing_enable(True)
 for _ in range(10):
     ls.sort_device(d, o, n, algo=algo, workspace=ws)
 torch.cuda.synchronize()
-row = {"lib": os.path.basename(os.environ.get("LABSORT_LIBRARY", "liblabsort.so")), "algo": algo}
+row = {"lib": os.path.basename(os.environ.get("LABSORT_LIBRARY", "liblabsort.so")), "algo": algo,
+       "ts_impl": os.environ.get("LABSORT_TS_IMPL", "")}
 for c in classes:
     ms, cnt = ls.timing_read(c)
     row[c + "_ms"] = round(ms / max(cnt, 1), 4)

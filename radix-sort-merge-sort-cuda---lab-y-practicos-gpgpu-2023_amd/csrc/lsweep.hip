@@ -68,8 +68,11 @@ __device__ __forceinline__ void ls_count_runs(uint32_t *jh, uint32_t f, bool ok,
     const uint32_t fp = __shfl_up(f, 1);
     const bool lead = ok && (lane == 0 || f != fp);
     const uint64_t L = __ballot(lead);
+    // (both ballots with the whole wave active: a ballot inside the select below would be
+    // compiled into its divergent arm and count only the lanes that take it)
+    const uint32_t nok = (uint32_t)__popcll(__ballot(ok));
     const uint64_t after = L & ~((2ull << lane) - 1ull);  // leaders after this lane (lane 63: none)
-    const uint32_t next = after ? (uint32_t)__builtin_ctzll(after) : (uint32_t)__popcll(__ballot(ok));
+    const uint32_t next = after ? (uint32_t)__builtin_ctzll(after) : nok;
     if (lead) atomicAdd(jh + f, next - lane);
 }
 __device__ __forceinline__ bool ls_repeats(uint32_t f) {

@@ -51,12 +51,14 @@ def test_wave_tile_sort(ls, oracle, torch_gpu, key, dist):
 
 # ---- LDS tile sort (stage 1+2 counterpart) ---------------------------------------------
 @pytest.mark.parametrize("key", ["u32", "i32"])
-@pytest.mark.parametrize("dist", ["u32", "mod100", "const", "lowbits"])
-def test_tile_sort(ls, oracle, torch_gpu, key, dist):
+@pytest.mark.parametrize("dist,param", [("u32", 0), ("mod100", 0), ("const", 0), ("lowbits", 9), ("lowbits", 12),
+                                        ("lowbits", 23), ("sorted", 0), ("reversed", 0)])
+def test_tile_sort(ls, oracle, torch_gpu, key, dist, param):
+    """Every tile sorted; lowbits 12 / 23 put the varying bits across a digit boundary."""
     torch = torch_gpu
     T = ls.tile_keys()
     n = 5 * T + 1234
-    a = oracle.gen(n, SEED + 3, dist, param=9)
+    a = oracle.gen(n, SEED + 3, dist, param=param)
     t = to_dev(torch, a)
     o = torch.empty_like(t)
     ls.tile_sort(t, o, n, key=key)
