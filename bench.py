@@ -620,7 +620,6 @@ def main():
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     k_ms, k_cnt = ls.timing_read(dom)
-    l_ms, l_cnt = ls.timing_read("lsweep")  # the local first pass (onesweep radix)
     ls.timing_enable(False)
     elapsed = t1 - t0
     status()
@@ -805,13 +804,6 @@ def main():
                                                else f"k_{dom}"), "launches": k_cnt,
                 "avg_launch_ms": round(avg_ms, 5) if avg_ms else None,
                 "algorithmic_bytes_per_launch": per_launch_bytes, "traffic_source": tsrc}
-    if l_cnt:  # the local pass: 8 B/key too (each key read and written once, contiguously)
-        lavg = l_ms / l_cnt
-        roofline["local_pass"] = {"kernel": "k_lsweep", "launches": l_cnt, "avg_launch_ms": round(lavg, 5),
-                                  "achieved": round(8.0 * n / (lavg * 1e-3) / 1e9, 1),
-                                  "frac": round(8.0 * n / (lavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                                  "copy_frac": round(8.0 * n / (lavg * 1e-3) / 1e9 / copy_gbs, 4),
-                                  "traffic": pmc_traffic("lsweep", n)[0]}
     roofline["copy_ceiling"] = {
         "value": round(copy_gbs, 1), "unit": "GB/s", "frac": round(achieved / copy_gbs, 4) if achieved else None,
         "ms": round(copy_ms, 5), "verified": bool(copy_ok),

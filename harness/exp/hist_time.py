@@ -12,7 +12,7 @@ d = torch.empty(n, dtype=torch.int32, device="cuda")
 ls.fill(d, n, 0x5EED0003, os.environ.get("DIST", "u32"))
 o = torch.empty_like(d)
 algo = os.environ.get("ALGO", "radix")
-classes = ("lsweep", "histogram", "onesweep") if algo == "radix" else ("tile_sort", "merge")
+classes = ("histogram", "onesweep") if algo == "radix" else ("tile_sort", "merge")
 ws = torch.empty(ls.workspace_bytes(n, algo), dtype=torch.uint8, device="cuda")
 for _ in range(3):
     ls.sort_device(d, o, n, algo=algo, workspace=ws)

@@ -1,4 +1,9 @@
-// lsweep.hip -- the local first pass of the 8-bit LSD radix sort (keys only, onesweep path).
+// lsweep_exp.hip -- EXPERIMENT, not in the product (r28): the local first pass of the 8-bit
+// LSD radix sort (keys only, onesweep path).  It ran in the product for one build with the
+// gathering first onesweep pass (kernels.hip at commit 4cccab1): correct on 479 radix GPU
+// tests, but 2.417 ms per 2^28 sort against 2.127 ms for the histogram path (k_lsweep
+// 0.642 ms, the gathering pass 0.785 ms), so the histogram path was
+// restored.  Kept for harness/exp/lsweep_probe.hip.
 //
 // The onesweep pass (kernels.hip, k_onesweep_p) needs every digit's global offset before
 // it scatters, so the classic design reads the keys once more up front (k_hist_seg:
@@ -24,10 +29,16 @@
 // global scan and scatter; here a tile is split by 8 bits at once and the scatter of the
 // first pass is deferred to the second pass's gather.
 #include "../../include/labsort.h"
-#include "common.h"
-#include "devutil.h"
+#include "../../radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd/csrc/common.h"
+#include "../../radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd/csrc/devutil.h"
 
 namespace labsort {
+
+constexpr int LS_BLOCK = 1024, LS_KPT = 16, LS_TILE = LS_BLOCK * LS_KPT;
+constexpr int LS_GROUP = 64;  // tiles per k_lscan workgroup
+struct GthTables {            // k_lscan's run tables (ls, sr: digit-major; first: per tile)
+    uint32_t *ls, *sr, *first;
+};
 
 namespace {
 

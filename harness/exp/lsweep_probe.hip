@@ -2,7 +2,7 @@
 // against a tiled 16-B copy of the same bytes (joint-field counting included),
 // for uniform / sorted / %100 / %1000 keys, and checks a few tiles on the host.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o lsweep_probe lsweep_probe.hip
-#include "../../radix-sort-merge-sort-cuda---lab-y-practicos-gpgpu-2023_amd/csrc/lsweep.hip"
+#include "lsweep_exp.hip"
 
 #include <algorithm>
 #include <cstdio>

@@ -80,9 +80,8 @@ extern "C" {
 #define LABSORT_K_PARTITION 4
 #define LABSORT_K_GSWEEP 5       /* gathered radix pass (LABSORT_ALGO_RADIX, 2^16 <= n < 2^25) */
 #define LABSORT_K_GCOPY 6        /* its final gathered copy */
-#define LABSORT_K_LSWEEP 7       /* the local first pass of the onesweep radix (k_lsweep) */
-#define LABSORT_K_COPY 8         /* the streaming copy (labsort_copy: the bench's copy ceiling) */
-#define LABSORT_K_COUNT 9
+#define LABSORT_K_COPY 7         /* the streaming copy (labsort_copy: the bench's copy ceiling) */
+#define LABSORT_K_COUNT 8
 
 /* ---- library info ---- */
 const char *labsort_version(void);

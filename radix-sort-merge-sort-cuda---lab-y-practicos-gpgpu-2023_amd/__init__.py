@@ -31,7 +31,7 @@ ALGO = {"radix": 0, "merge": 1, "radix1": 2, "auto": 3}
 KEY = {"u32": 0, "i32": 1}
 DIST = {"u32": 0, "u31": 1, "mod100": 2, "mod1000": 3, "sorted": 4, "reversed": 5, "const": 6, "lowbits": 7}
 KCLASS = {"histogram": 0, "onesweep": 1, "tile_sort": 2, "merge": 3, "partition": 4, "gsweep": 5, "gcopy": 6,
-          "lsweep": 7, "copy": 8}
+          "copy": 7}
 
 # exported symbols of include/labsort.h + lab.h (checked by tests/test_abi.py)
 C_SYMBOLS = [
@@ -414,7 +414,7 @@ GS_MIN_N, GS_MAX_N = 1 << 16, 1 << 25  # LABSORT_ALGO_RADIX's gathered-pass wind
 
 def radix_impl(n: int) -> str:
     """Which LSD implementation LABSORT_ALGO_RADIX runs for n keys: "gather" (gsweep.hip)
-    or "onesweep" (lsweep.hip + kernels.hip), as api.hip's use_gather decides."""
+    or "onesweep" (kernels.hip), as api.hip's use_gather decides."""
     env = os.environ.get("LABSORT_RADIX_IMPL", "")
     if env == "gather":
         return "gather"

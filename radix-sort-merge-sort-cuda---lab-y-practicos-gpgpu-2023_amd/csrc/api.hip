@@ -129,59 +129,6 @@ RadixLayout radix_layout(size_t n, int bits, size_t tile) {
     return L;
 }
 
-// The keys-only 8-bit radix (the local-pass path, lsweep.hip): zeroed header (error word,
-// digit-0 totals, joint fields, acquisition counters of the 3 launches, k_lscan's group
-// counter and look-back flags), the 3 launches' look-back words (cleared by the plan
-// launch), plan and segment plans, the local pass's tile rows, the run tables, and two
-// key buffers (TMP: the local pass's output; TMP2: between the later launches).
-struct LLayout {
-    size_t ntp, ng, ntiles;
-    size_t off_err, off_tot0, off_joint, off_counter, off_gctr, off_flags, zero_bytes;
-    size_t off_lookback, lb_end, off_plan, off_segplan, off_hist, off_rows, off_ls, off_sr, off_first, off_tmp,
-        off_tmp2, total;
-};
-LLayout l_layout(size_t n) {
-    LLayout L{};
-    L.ntp = (n + OSP_TILE - 1) / OSP_TILE;
-    L.ng = (L.ntp + LS_GROUP - 1) / LS_GROUP;
-    L.ntiles = L.ntp + NSEG;  // look-back slots per launch (tiles + one partial tile per segment)
-    size_t o = 0;
-    L.off_err = o;
-    o += 256;
-    L.off_tot0 = o;
-    o += 256 * 4;
-    L.off_joint = o;
-    o += (size_t)4 * NSEG * 256 * 4;
-    L.off_counter = o;
-    o += (size_t)3 * OSP_NCTR * 4;
-    L.off_gctr = o;
-    o = align_up(o + 4, 256);
-    L.off_flags = o;
-    o = align_up(o + L.ng * 256 * 4, 256);
-    L.zero_bytes = o;
-    L.off_lookback = o;
-    o = align_up(o + (size_t)3 * L.ntiles * 256 * 4, 256);
-    L.lb_end = o;
-    L.off_plan = o;
-    o = align_up(o + sizeof(Plan), 256);
-    L.off_segplan = o;
-    o = align_up(o + 3 * sizeof(SegPlan), 256);
-    L.off_hist = o;
-    o = align_up(o + 4 * 256 * 4, 256);
-    L.off_rows = o;
-    o = align_up(o + L.ntp * 256 * 4, 256);
-    L.off_ls = o;
-    o = align_up(o + (256 * L.ntp + 1) * 4, 256);
-    L.off_sr = o;
-    o = align_up(o + 256 * L.ntp * 4, 256);
-    L.off_first = o;
-    o = align_up(o + (L.ntp + 1) * 4, 256);
-    L.off_tmp = align_up(o, 65536);  // key buffers 64 KiB aligned (tiles are 64 KiB of keys)
-    L.off_tmp2 = align_up(L.off_tmp + n * 4, 65536);
-    L.total = align_up(L.off_tmp2 + n * 4, 256);
-    return L;
-}
-
 struct MergeLayout {
     size_t off_tmp, off_part, total;
 };
@@ -232,67 +179,52 @@ void hook_end(void *ctx, int cls, hipStream_t s) {
 
 bool small_path(size_t n, int algo) { return algo != LABSORT_ALGO_RADIX1 && n <= (size_t)TS_TILE; }
 
-// LABSORT_ALGO_RADIX1: letra.pdf's 1-bit split passes (32 of them): the digit histogram,
-// the plan, the non-persistent look-back passes, the final copy
-int sort_radix1(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s) {
-    const RadixLayout L = radix_layout(n, 1, OS_TILE);
+int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int bits, char *ws, hipStream_t s) {
+    const RadixLayout L = radix_layout(n, bits, bits == 8 ? OSP_TILE : OS_TILE);
     Bufs b;
     b.p[SEL_IN] = const_cast<uint32_t *>(in);
     b.p[SEL_OUT] = out;
     b.p[SEL_TMP] = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
-    b.p[SEL_TMP2] = nullptr;
     uint32_t *hist = reinterpret_cast<uint32_t *>(ws + L.off_hist);
     uint32_t *counters = reinterpret_cast<uint32_t *>(ws + L.off_counter);
     uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
     uint32_t *lookback = reinterpret_cast<uint32_t *>(ws + L.off_lookback);
     Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
-    HIP_TRY(launch_zero(ws, L.zero_bytes, s));
-    {
-        TimingScope ts(LABSORT_K_HISTOGRAM, s);
-        HIP_TRY(launch_histogram(in, n, flip, 1, hist, s));
+    if (bits == 8) {
+        // histograms first; the look-back words (tens of MB) are cleared after the
+        // histogram so their dirty lines do not compete with its read of the keys
+        HIP_TRY(launch_zero(ws, L.off_lookback, s));
+        uint32_t *hps = reinterpret_cast<uint32_t *>(ws + L.off_hps);
+        uint32_t *joint = reinterpret_cast<uint32_t *>(ws + L.off_joint);
+        SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
+        {
+            TimingScope ts(LABSORT_K_HISTOGRAM, s);
+            HIP_TRY(launch_hist_seg(in, n, flip, hps, joint, s));
+        }
+        // the look-back clear rides in the plan launch (k_plan8's workgroups 1..)
+        HIP_TRY(launch_plan8(hps, joint, n, in == out ? 1 : 0, plan, sps, hist, ws + L.off_lookback,
+                             L.zero_bytes - L.off_lookback, s));
+        for (int p = 0; p < L.P; ++p) {
+            TimingScope ts(LABSORT_K_ONESWEEP, s);
+            HIP_TRY(launch_onesweep_p(b, plan, p, n, flip, sps + p, lookback + (size_t)p * L.ntiles * L.R,
+                                      counters + (size_t)p * OSP_NCTR, err, s));
+        }
+    } else {
+        HIP_TRY(launch_zero(ws, L.zero_bytes, s));
+        {
+            TimingScope ts(LABSORT_K_HISTOGRAM, s);
+            HIP_TRY(launch_histogram(in, n, flip, bits, hist, s));
+        }
+        HIP_TRY(launch_plan(hist, n, bits, in == out ? 1 : 0, plan, s));
+        for (int p = 0; p < L.P; ++p) {
+            TimingScope ts(LABSORT_K_ONESWEEP, s);
+            HIP_TRY(launch_onesweep(b, plan, p, bits, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
+                                    counters + (size_t)p * OSP_NCTR, err, s));
+        }
     }
-    HIP_TRY(launch_plan(hist, n, 1, in == out ? 1 : 0, plan, s));
-    for (int p = 0; p < L.P; ++p) {
-        TimingScope ts(LABSORT_K_ONESWEEP, s);
-        HIP_TRY(launch_onesweep(b, plan, p, 1, n, flip, hist, lookback + (size_t)p * L.ntiles * L.R,
-                                counters + (size_t)p * OSP_NCTR, err, s));
-    }
-    HIP_TRY(launch_final_copy(b, plan, n, s));
-    return LABSORT_OK;
-}
-
-// The keys-only 8-bit LSD radix (lsweep.hip): the local pass sorts every
-// tile by digit 0 in place of the upfront histogram read and the first scatter, and
-// counts what the later passes' segment plans need; k_lscan turns its tile rows into the
-// run tables of its logical order; the plan launch marks the digits 1-3 that vary and
-// clears the look-back words; launch 0 gathers its tiles through the run tables, launches
-// 1-2 read contiguously; k_lcopy gathers the result when no digit after 0 varies.
-int sort_radix8(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s) {
-    const LLayout L = l_layout(n);
-    Bufs b;
-    b.p[SEL_IN] = const_cast<uint32_t *>(in);
-    b.p[SEL_OUT] = out;
-    b.p[SEL_TMP] = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
-    b.p[SEL_TMP2] = reinterpret_cast<uint32_t *>(ws + L.off_tmp2);
-    auto at = [&](size_t off) { return reinterpret_cast<uint32_t *>(ws + off); };
-    uint32_t *err = at(L.off_err), *tot0 = at(L.off_tot0), *joint = at(L.off_joint), *counters = at(L.off_counter);
-    uint32_t *lookback = at(L.off_lookback), *rows = at(L.off_rows);
-    Plan *plan = reinterpret_cast<Plan *>(ws + L.off_plan);
-    SegPlan *sps = reinterpret_cast<SegPlan *>(ws + L.off_segplan);
-    const GthTables tb{at(L.off_ls), at(L.off_sr), at(L.off_first)};
-    HIP_TRY(launch_zero(ws, L.zero_bytes, s));
-    {
-        TimingScope ts(LABSORT_K_LSWEEP, s);
-        HIP_TRY(launch_lsweep(in, b.p[SEL_TMP], n, flip, rows, tot0, joint, s));
-    }
-    HIP_TRY(launch_lscan(rows, tot0, at(L.off_flags), at(L.off_gctr), err, tb, n, s));
-    HIP_TRY(launch_plan_l(tot0, joint, n, plan, sps, at(L.off_hist), ws + L.off_lookback, L.lb_end - L.off_lookback, s));
-    for (int j = 0; j < 3; ++j) {
-        TimingScope ts(LABSORT_K_ONESWEEP, s);
-        HIP_TRY(launch_onesweep_p(b, plan, j, n, flip, sps + j, lookback + (size_t)j * L.ntiles * 256,
-                                  counters + (size_t)j * OSP_NCTR, err, s, nullptr, j == 0 ? &tb : nullptr));
-    }
-    HIP_TRY(launch_lcopy(b, plan, tb, n, s));
+    // 8-bit: pass 0's launch copies an input whose every digit is constant (IN -> OUT), so
+    // only an in-place sort (its odd pass count ends in TMP) needs the final copy launch
+    if (bits != 8 || in == out) HIP_TRY(launch_final_copy(b, plan, n, s));
     return LABSORT_OK;
 }
 
@@ -402,7 +334,7 @@ int resolve_pairs_algo(int algo, size_t n) {
 // (labsort_sort_host's ragged last chunk, a rank's smaller shard) whichever
 // implementation that length selects.
 size_t radix_ws_bytes(size_t n) {
-    size_t w = l_layout(n).total;
+    size_t w = radix_layout(n, 8, OSP_TILE).total;
     if (n >= GS_MIN_N) {
         const size_t g = gs_layout(n < GS_MAX_N ? n : GS_MAX_N - 1).total;
         w = g > w ? g : w;
@@ -529,7 +461,7 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
         HIP_TRY(launch_gsweep_sort(in, out, n, flip, ws, s, GsHooks{&hc, hook_begin, hook_end}));
         return LABSORT_OK;
     }
-    return algo == LABSORT_ALGO_RADIX1 ? sort_radix1(in, out, n, flip, ws, s) : sort_radix8(in, out, n, flip, ws, s);
+    return sort_radix(in, out, n, flip, algo == LABSORT_ALGO_RADIX1 ? 1 : 8, ws, s);
 }
 
 namespace {
@@ -787,7 +719,7 @@ namespace {
 int sort_pairs_radix(const uint32_t *ki, const uint32_t *vi, uint32_t *ko, uint32_t *vo, size_t n, uint32_t flip,
                      char *ws, hipStream_t s) {
     const RadixLayout L = radix_layout(n, 8, OSP_TILE);
-    Bufs b{}, vb{};
+    Bufs b, vb;
     b.p[SEL_IN] = const_cast<uint32_t *>(ki);
     b.p[SEL_OUT] = ko;
     b.p[SEL_TMP] = reinterpret_cast<uint32_t *>(ws + L.off_tmp);

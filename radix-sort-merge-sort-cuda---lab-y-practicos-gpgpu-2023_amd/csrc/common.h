@@ -35,12 +35,6 @@ constexpr int NT_LOADS = NT_OSP | NT_HIST;
 constexpr int OSP_NCTR = 8;  // tile acquisition counters per pass: one per XCD group of segments
 static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass tiles");
 
-// ---- local first pass (lsweep.hip): tiles sorted by digit 0 in place, rows of counts ----
-constexpr int LS_BLOCK = 1024, LS_KPT = 16, LS_TILE = LS_BLOCK * LS_KPT;
-hipError_t launch_lsweep(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, uint32_t *rows, uint32_t *tot0,
-                         uint32_t *joint, hipStream_t s);
-constexpr int LS_GROUP = 64;  // tiles per k_lscan workgroup
-
 // ---- segmented look-back chains (8-bit radix) ----
 // Each pass's input is split into NSEG contiguous segments, each with its own
 // decoupled look-back chain; a segment's base offsets come from histograms the
@@ -114,7 +108,7 @@ hipError_t launch_gsweep_sort(const uint32_t *in, uint32_t *out, size_t n, uint3
                               const GsHooks &hooks);
 
 constexpr int MAX_PASSES = 32;
-constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_TMP2 = 3, SEL_SKIP = 0xFFu;
+constexpr uint32_t SEL_IN = 0, SEL_OUT = 1, SEL_TMP = 2, SEL_SKIP = 0xFFu;
 constexpr uint32_t SPIN_LIMIT = 1u << 22;  // bounded look-back spins: past it the error word is set
 constexpr uint32_t NEXT_NONE = 0xFFFFFFFFu;
 
@@ -127,22 +121,13 @@ struct Plan {
     uint32_t dst[MAX_PASSES];
     uint32_t next[MAX_PASSES];  // 8-bit radix: next active pass after this one (NEXT_NONE)
     uint32_t prev[MAX_PASSES];  // 8-bit radix: previous active pass (NEXT_NONE for the first)
-    uint32_t digit[MAX_PASSES]; // 8-bit radix: the digit launch p sorts by (the histogram path:
-                                // p; the local-pass path: its p-th active digit after digit 0)
     uint32_t copy_from;  // SEL_SKIP: result already in OUT
     uint32_t active;     // number of non-trivial passes
     uint32_t pad[2];
 };
 
 struct Bufs {
-    uint32_t *p[4];  // IN, OUT, TMP, TMP2
-};
-
-// Run tables of the local pass's logical order (lsweep.hip k_lscan): run e = d * ntp + t
-// starts at logical position ls[e] and address sr[e]; first[T] = the run holding position
-// T * OSP_TILE (first[ntp]: position n - 1); ls[256 ntp] = n
-struct GthTables {
-    const uint32_t *ls, *sr, *first;
+    uint32_t *p[3];  // IN, OUT, TMP
 };
 
 // lookback word: 2 status bits + 30-bit count (n < 2^30 per radix sort)
@@ -166,13 +151,7 @@ hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, in
                         SegPlan *segplans, uint32_t *hist, void *zero_p, size_t zero_bytes, hipStream_t s);
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
                              uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s,
-                             const Bufs *vb = nullptr, const GthTables *tb = nullptr);
-// the local-pass path (lsweep.hip): run tables, plan (+ the look-back clear), gathered copy
-hipError_t launch_lscan(const uint32_t *rows, const uint32_t *tot0, uint32_t *flags, uint32_t *gctr, uint32_t *err,
-                        GthTables tb, size_t n, hipStream_t s);
-hipError_t launch_plan_l(const uint32_t *tot0, const uint32_t *joint, size_t n, Plan *plan, SegPlan *segplans,
-                         uint32_t *hist, void *zero_p, size_t zero_bytes, hipStream_t s);
-hipError_t launch_lcopy(Bufs b, const Plan *plan, GthTables tb, size_t n, hipStream_t s);
+                             const Bufs *vb = nullptr);
 hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s);
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s);
 hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStream_t s);

@@ -443,7 +443,6 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
             plan->dst[p] = SEL_SKIP;
             plan->next[p] = NEXT_NONE;
             plan->prev[p] = NEXT_NONE;
-            plan->digit[p] = (uint32_t)p;
         }
         for (int p = 0; p < 4; ++p) {
             prevs[p] = NEXT_NONE;
@@ -494,77 +493,6 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
         if (prevs[q] == NEXT_NONE) continue;  // (block-uniform)
         __syncthreads();  // sh, start reused
         build_segplan_later(sps + q, q, prevs[q], n, seg_later, hist, joint, sh, start);
-    }
-}
-
-// Plan of the local-pass path (lsweep.hip): the local pass has sorted every tile by
-// digit 0 (its logical order is digit-0 order), so the launches that follow sort by the
-// active digits among 1..3: launch j by digit[j], reading TMP (the local pass's output,
-// gathered through the run tables) for j = 0 and the previous launch's output after it,
-// the last one writing OUT (TMP2 and TMP in between, so a launch never reads the buffer it
-// writes, in place or not).  With no active digit the logical order is the sorted array
-// and k_lcopy gathers it into OUT (copy_from = TMP).  Segments: as in k_plan8, with the
-// local pass's digit 0 as the previous digit of launch 0.  hist_out: the 4 digit
-// histograms (digit 0 = tot0, digits 1-3 = the joint marginals).  Workgroups 1.. clear the
-// look-back region (zp, zn4 uint4s) meanwhile.
-__global__ __launch_bounds__(256) void k_plan_l(const uint32_t *__restrict__ tot0, const uint32_t *__restrict__ joint,
-                                                uint32_t n, Plan *__restrict__ plan, SegPlan *__restrict__ sps,
-                                                uint32_t *__restrict__ hist_out, uint4 *__restrict__ zp, size_t zn4) {
-    if (blockIdx.x > 0) {
-        const size_t stride = (size_t)(gridDim.x - 1) * blockDim.x;
-        for (size_t i = (size_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < zn4; i += stride)
-            zp[i] = make_uint4(0u, 0u, 0u, 0u);
-        return;
-    }
-    __shared__ uint32_t hist[4 * 256];
-    __shared__ uint32_t sh[NSEG * 256 + 8];
-    __shared__ uint32_t start[NSEG + 1];
-    __shared__ uint32_t triv[4], act[3], nact;
-    const uint32_t t = threadIdx.x;
-    if (t < 4) triv[t] = 0;
-    __syncthreads();
-    uint32_t v[4] = {tot0[t], 0u, 0u, 0u};
-    for (int s = 0; s < NSEG; ++s) {
-#pragma unroll
-        for (int p = 1; p < 4; ++p) v[p] += joint[(p * NSEG + s) * 256 + t];  // marginal over the nibble
-    }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        hist[p * 256 + t] = v[p];
-        hist_out[p * 256 + t] = v[p];
-        if (v[p] == n) triv[p] = 1;
-    }
-    __syncthreads();
-    if (t == 0) {
-        uint32_t k = 0;
-        for (int p = 1; p < 4; ++p)
-            if (!triv[p]) act[k++] = (uint32_t)p;
-        nact = k;
-        for (int j = 0; j < MAX_PASSES; ++j) {
-            plan->src[j] = SEL_SKIP;
-            plan->dst[j] = SEL_SKIP;
-            plan->next[j] = NEXT_NONE;
-            plan->prev[j] = NEXT_NONE;
-            plan->digit[j] = 0;
-        }
-        uint32_t src = SEL_TMP;
-        for (uint32_t j = 0; j < k; ++j) {
-            const uint32_t dst = j + 1 == k ? SEL_OUT : (j % 2 == 0 ? SEL_TMP2 : SEL_TMP);
-            plan->src[j] = src;
-            plan->dst[j] = dst;
-            plan->digit[j] = act[j];
-            plan->prev[j] = j ? act[j - 1] : 0u;
-            plan->next[j] = j + 1 < k ? act[j + 1] : NEXT_NONE;
-            src = dst;
-        }
-        plan->active = k;
-        plan->copy_from = k ? SEL_SKIP : SEL_TMP;
-    }
-    __syncthreads();
-    const uint32_t k = nact;
-    for (uint32_t j = 0; j < k; ++j) {
-        __syncthreads();  // sh, start reused
-        build_segplan_later(sps + j, (int)act[j], j ? act[j - 1] : 0u, n, 1, hist, joint, sh, start);
     }
 }
 
@@ -748,129 +676,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t osp_rsrc(const uint32_t *p, ui
 }
 constexpr int OSP_BUF_NT = (NT_LOADS & NT_OSP) ? 2 : 0;  // aux bit 1 = nontemporal
 
-// ---- gathered tile loads: the first onesweep pass after the local pass (lsweep.hip) ----
-// Its logical input is the local pass's digit-0 order: run e = (digit d, tile t) of ~64
-// keys at address sr[e], logical start ls[e] (k_lscan's tables).  Per tile the runs that
-// meet it are marked in LDS -- a 64-bit start mask per 64-position block and the
-// blocks' prefix counts -- with each marked run's delta (source - logical position), so a
-// key slot (64 consecutive positions = one block) finds every lane's source address with
-// one broadcast LDS read, a popcount and one delta read, and the 16 loads of a lane issue
-// back to back.  More than GTH_KMAX runs in one tile (rare: many tiny digit-0 runs):
-// each lane searches the tables instead.
-constexpr int GTH_KMAX = 1024;
-struct GthS {
-    uint64_t mask[OSP_TILE / 64];  // run-start bits of each 64-position block of the tile
-    uint32_t pre[OSP_TILE / 64];   // set bits in the blocks before
-    int32_t delta[GTH_KMAX];       // per marked run, in order: source address - logical position
-    uint32_t over, e0, e1, pad;    // over: the slow path (per-lane table search over runs e0..e1)
-};
-struct GthPair {
-    GthS s[2];  // the next tile's structure is built while the current one's is used
-};
-struct GthNone {};
-
-// first run index e0 and last e1 of logical tile range [L0, L0 + nv) (inside the aligned
-// logical tile L0 / OSP_TILE)
-__device__ __forceinline__ void gth_range(const GthTables &tb, uint32_t L0, uint32_t &e0, uint32_t &e1) {
-    const uint32_t k = L0 / (uint32_t)OSP_TILE;
-    e0 = tb.first[k];
-    e1 = tb.first[k + 1];
-}
-// run entry `tid` of runs e0..e1: start a, end b (the next run's start), source s
-__device__ __forceinline__ void gth_run(const GthTables &tb, uint32_t e0, uint32_t e1, uint32_t tid, uint32_t &a,
-                                        uint32_t &b, uint32_t &s) {
-    a = b = s = 0u;
-    if (e1 - e0 < (uint32_t)GTH_KMAX && tid <= e1 - e0) {
-        a = tb.ls[e0 + tid];
-        b = tb.ls[e0 + tid + 1];
-        s = tb.sr[e0 + tid];
-    }
-}
-__device__ __forceinline__ bool gth_meets(uint32_t a, uint32_t b, uint32_t L0, uint32_t nv) {
-    return b > a && b > L0 && a < L0 + nv;
-}
-// (after the clear and a barrier) mark the start of a run that meets the tile
-__device__ __forceinline__ void gth_mark(GthS &S, uint32_t a, uint32_t b, uint32_t L0, uint32_t nv) {
-    if (gth_meets(a, b, L0, nv)) {
-        const uint32_t rel = a > L0 ? a - L0 : 0u;
-        atomicOr(reinterpret_cast<unsigned long long *>(&S.mask[rel >> 6]), 1ull << (rel & 63u));
-    }
-}
-// (one wave, after a barrier) the blocks' prefix counts, 4 blocks per lane
-__device__ __forceinline__ void gth_prefix(GthS &S, uint32_t lane) {
-    static_assert(OSP_TILE / 64 == 4 * WAVE, "4 blocks per lane");
-    uint32_t c[4], sum = 0;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        c[i] = (uint32_t)__popcll(S.mask[4 * lane + i]);
-        sum += c[i];
-    }
-    uint32_t x = sum;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_up(x, off);
-        if (lane >= (uint32_t)off) x += y;
-    }
-    uint32_t e = x - sum;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        S.pre[4 * lane + i] = e;
-        e += c[i];
-    }
-}
-// (after a barrier) the marked run's delta at its rank among the marked runs
-__device__ __forceinline__ void gth_delta(GthS &S, uint32_t a, uint32_t b, uint32_t s, uint32_t L0, uint32_t nv) {
-    if (gth_meets(a, b, L0, nv)) {
-        const uint32_t rel = a > L0 ? a - L0 : 0u, blk = rel >> 6;
-        const uint32_t r = S.pre[blk] + (uint32_t)__popcll(S.mask[blk] & ((1ull << (rel & 63u)) - 1ull));
-        S.delta[r] = (int32_t)(s - a);
-    }
-}
-// keys of logical tile [L0, L0 + nv) in the wave's blocked layout (slot j of wave w = the
-// 64 positions of block w * KPT + j); sentinels past nv
-template <int KPT>
-__device__ __forceinline__ void gth_load(const GthS &S, const GthTables &tb, __amdgpu_buffer_rsrc_t rin, uint32_t L0,
-                                         uint32_t nv, uint32_t wid, uint32_t lane, uint32_t sentinel, int nt,
-                                         uint32_t (&k)[KPT]) {
-    if (!S.over) {
-        uint32_t addr[KPT];
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t blk = wid * KPT + (uint32_t)j, p = blk * 64u + lane;
-            const uint64_t m = S.mask[blk];  // (one address per wave: a broadcast read)
-            const uint32_t r = S.pre[blk] + (uint32_t)__popcll(m & ((2ull << lane) - 1ull)) - 1u;
-            addr[j] = L0 + p + (uint32_t)S.delta[r < (uint32_t)GTH_KMAX ? r : 0u];
-        }
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            // (nontemporal policy bits as the plain loads; past nv the address is garbage
-            // and the key replaced: buffer loads out of range return 0)
-            const uint32_t v = nt ? __builtin_amdgcn_raw_buffer_load_b32(rin, addr[j] * 4u, 0, 2)
-                                  : __builtin_amdgcn_raw_buffer_load_b32(rin, addr[j] * 4u, 0, 0);
-            k[j] = (wid * KPT + (uint32_t)j) * 64u + lane < nv ? v : sentinel;
-        }
-    } else {
-        // many (mostly tiny) runs: each lane searches the run starts for its positions
-#pragma unroll 1
-        for (int j = 0; j < KPT; ++j) {
-            const uint32_t p = (wid * KPT + (uint32_t)j) * 64u + lane;
-            uint32_t v = sentinel;
-            if (p < nv) {
-                const uint32_t P = L0 + p;
-                uint32_t lo = S.e0, hi = S.e1 + 1u;  // ls[lo] <= P < ls[hi]
-                while (hi - lo > 1u) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (tb.ls[mid] <= P) lo = mid;
-                    else hi = mid;
-                }
-                v = __builtin_amdgcn_raw_buffer_load_b32(rin, (tb.sr[lo] + (P - tb.ls[lo])) * 4u, 0, 0);
-            }
-            k[j] = v;
-        }
-    }
-}
-
-template <bool KV, bool GATHER = false>
+template <bool KV>
 struct OspSmem {
     static constexpr int BLOCK = KV ? OSP_KV_BLOCK : OSP_BLOCK;  // threads (key/value: its own shape)
     static constexpr int R = 256, W = BLOCK / WAVE, TILE = OSP_TILE;
@@ -885,8 +691,7 @@ struct OspSmem {
     uint32_t start[NSEG + 1];
     uint32_t tpre[NSEG + 1];
     uint32_t wsum[8];
-    uint32_t next, next2, next3;
-    std::conditional_t<GATHER, GthPair, GthNone> g;  // gathered loads: two run structures
+    uint32_t next, next2;
 };
 
 constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
@@ -896,18 +701,11 @@ constexpr uint32_t OSP_DONE = 0xFFFFFFFFu;
 // its key's destination.  No room in LDS for the match buffer (the rank's fallback is
 // then 8 ballots) nor the bases table, and no registers for the next tile's prefetch:
 // 512-thread workgroups, the acquisition at the end of the iteration.
-// GATHER: the first launch after the local pass (lsweep.hip): tile C's keys are gathered
-// through the run tables tb (gth_load); tile D's run structure is built during the
-// iteration before (its table entries loaded at the top, marked after barrier 2, its
-// prefix counts after 2b by the last wave, its deltas after 3), so three tiles are
-// acquired ahead (B, C, D) instead of two.
-template <bool KV = false, bool GATHER = false>
+template <bool KV = false>
 __global__ __launch_bounds__(KV ? OSP_KV_BLOCK : OSP_BLOCK, (KV ? OSP_KV_BLOCK : OSP_BLOCK) / 256)
 void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n, uint32_t flip,
-                  const SegPlan *__restrict__ sp, uint32_t *lookback, uint32_t *counter, uint32_t *err, Bufs vbufs,
-                  GthTables tb) {
-    static_assert(!(KV && GATHER), "key/value sorts take the histogram path");
-    using S = OspSmem<KV, GATHER>;
+                  const SegPlan *__restrict__ sp, uint32_t *lookback, uint32_t *counter, uint32_t *err, Bufs vbufs) {
+    using S = OspSmem<KV>;
     constexpr bool PF = !KV;  // next tile's keys loaded one iteration ahead
     constexpr bool ST4 = !KV;  // grouped 16-B scatter stores (r26; the key/value pass measured 2-5 % slower with them)
     constexpr int R = S::R, W = S::W, TILE = S::TILE, BLK = S::BLOCK, KPT = TILE / BLK, LBW = OSP_LBW;
@@ -934,7 +732,7 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
         return;
     }
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t shift = plan->digit[pass] * 8u;
+    const uint32_t shift = (uint32_t)pass * 8u;
     const uint32_t sentinel = ~flip;  // digit 255 in every pass: ranks after all real keys
     // tile id c = l * NSEG + segment (tile l of the segment)
     constexpr uint32_t segbits = 4, segmask = NSEG - 1;
@@ -995,14 +793,13 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
         const uint32_t c0 = acquire();
         sm.next = c0;
         sm.next2 = (PF && c0 != OSP_DONE) ? acquire() : OSP_DONE;
-        sm.next3 = (GATHER && sm.next2 != OSP_DONE) ? acquire() : OSP_DONE;
     }
     if (wid == 0) {
         const bool ord = lds_lane_ordered(sm.probe, lane);
         if (lane == 0) sm.ordered = ord ? 1u : 0u;
     }
     __syncthreads();
-    uint32_t cB = sm.next, cC = sm.next2, cD = sm.next3;
+    uint32_t cB = sm.next, cC = sm.next2;
     const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
 
     // carried state of tile A (slot = look-back slot, lo = slot of its segment's first tile)
@@ -1051,45 +848,7 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
     };
     uint32_t kB[KPT], kN[PF ? KPT : 1];
     uint32_t vB[KV ? KPT : 1];
-    uint32_t sc = 0;            // GATHER: the structure of tile C (D's is built in the other)
-    uint32_t e0D = 0, e1D = 0;  // GATHER: the run range of tile D
-    if constexpr (GATHER) {
-        // B's and C's run structures (once per workgroup, not pipelined), B's keys
-        auto build = [&](uint32_t c, GthS &G) {  // block-uniform
-            uint32_t L0 = 0, nv = 0, e0 = 0, e1 = 0, a = 0, b = 0, s = 0;
-            if (c != OSP_DONE) {
-                tile_range(c, L0, nv);
-                gth_range(tb, L0, e0, e1);
-                gth_run(tb, e0, e1, tid, a, b, s);
-            }
-            if (tid < (uint32_t)(OSP_TILE / 64)) G.mask[tid] = 0ull;
-            if (tid == 0) {
-                G.over = c != OSP_DONE && e1 - e0 >= (uint32_t)GTH_KMAX;
-                G.e0 = e0;
-                G.e1 = e1;
-            }
-            __syncthreads();
-            gth_mark(G, a, b, L0, nv);
-            __syncthreads();
-            if (wid == 0) gth_prefix(G, lane);
-            __syncthreads();
-            gth_delta(G, a, b, s, L0, nv);
-            __syncthreads();
-        };
-        build(cB, sm.g.s[0]);
-        if (cB != OSP_DONE) {
-            uint32_t beg, nv;
-            tile_range(cB, beg, nv);
-            gth_load<KPT>(sm.g.s[0], tb, rin, beg, nv, wid, lane, sentinel, OSP_BUF_NT, kN);
-        }
-        build(cC, sm.g.s[1]);
-        sc = 1;
-        if (cD != OSP_DONE) {
-            uint32_t beg, nv;
-            tile_range(cD, beg, nv);
-            gth_range(tb, beg, e0D, e1D);
-        }
-    } else if constexpr (PF) {
+    if constexpr (PF) {
         if (cB != OSP_DONE) load_tile(cB, kN);
     }
 
@@ -1100,7 +859,7 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
         }
         const bool haveB = cB != OSP_DONE;
         uint32_t acq_c = 0;  // tid 0: the early counter increment
-        const uint32_t cLast = GATHER ? cD : cC;  // the last tile acquired so far
+        const uint32_t cLast = cC;  // the last tile acquired so far
         if (PF && tid == 0 && cLast != OSP_DONE && gk < G) acq_c = atomicAdd(counter + ((home + gk) & (G - 1u)), 1u);
         const uint32_t segB = cB & segmask, lB = cB >> segbits;
         const uint32_t loB = haveB ? sm.tpre[segB] : 0u, slotB = loB + lB;
@@ -1115,32 +874,11 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
             for (int i = 0; i < LBW; ++i)
                 lwA[i] = (hi - i >= (int32_t)loA) ? ld_agent(lookback + (size_t)(hi - i) * R + tid) : LB_INC;
         }
-        if constexpr (GATHER) {
-            if (cC != OSP_DONE) {
-                uint32_t begC, nvC;
-                tile_range(cC, begC, nvC);
-                gth_load<KPT>(sm.g.s[sc], tb, rin, begC, nvC, wid, lane, sentinel, OSP_BUF_NT, kN);
-            }
-        } else if constexpr (PF) {
+        if constexpr (PF) {
             if (cC != OSP_DONE) load_tile(cC, kN);
         } else if (haveB) {
             load_tile(cB, kB);
             if constexpr (KV) load_vals(cB, vB);
-        }
-        // GATHER: tile D's run structure, step 1: clear, table entries
-        uint32_t La = 0, Lb = 0, Ls = 0, L0D = 0, nvD = 0;
-        if constexpr (GATHER) {
-            GthS &GD = sm.g.s[sc ^ 1u];
-            if (tid < (uint32_t)(OSP_TILE / 64)) GD.mask[tid] = 0ull;
-            if (tid == 0) {
-                GD.over = cD != OSP_DONE && e1D - e0D >= (uint32_t)GTH_KMAX;
-                GD.e0 = e0D;
-                GD.e1 = e1D;
-            }
-            if (cD != OSP_DONE) {
-                tile_range(cD, L0D, nvD);
-                gth_run(tb, e0D, e1D, tid, La, Lb, Ls);
-            }
         }
         if (haveB) {  // stable wave rank of B
 #pragma unroll
@@ -1208,7 +946,6 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
             sm.delta[tid] = (KV ? sp->base[segA * R + tid] : sm.base[segA * R + tid]) + excl - dstartA;
         }
         __syncthreads();  // (2) delta of A, wave counts of B
-        if constexpr (GATHER) gth_mark(sm.g.s[sc ^ 1u], La, Lb, L0D, nvD);  // D, step 2
         if (haveB && tid < (uint32_t)R) {
             // tile histogram = sum of the per-wave counts; publish B's aggregate, scan it
             uint32_t tot = 0;
@@ -1261,8 +998,6 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
         }
         if (!haveB) break;
         __syncthreads();  // (2b) wave sums of B's digit scan
-        if constexpr (GATHER)
-            if (wid == (uint32_t)W - 1u) gth_prefix(sm.g.s[sc ^ 1u], lane);  // D, step 3
         if (tid < (uint32_t)R) {
             uint32_t add = 0;
 #pragma unroll
@@ -1280,16 +1015,6 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
         }
         if (tid == 0) sm.next = !PF ? acquire() : cLast != OSP_DONE ? acquire_done(acq_c) : OSP_DONE;
         __syncthreads();  // (3) wave offsets of B
-        uint32_t e0N = 0, e1N = 0;
-        if constexpr (GATHER) {
-            gth_delta(sm.g.s[sc ^ 1u], La, Lb, Ls, L0D, nvD);  // D, step 4
-            const uint32_t cN = sm.next;  // the tile after D: its run range (used next iteration)
-            if (cN != OSP_DONE) {
-                uint32_t beg, nv;
-                tile_range(cN, beg, nv);
-                gth_range(tb, beg, e0N, e1N);
-            }
-        }
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t pos = osp_pad(wh[((kB[j] ^ flip) >> shift) & 255u] + ((rB[j / 2] >> ((j & 1) * 16)) & 0xFFFFu));
@@ -1316,53 +1041,12 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
         segA = segB;
         nvalidA = nvalidB;
         aggA = hB;
-        if constexpr (GATHER) {
-            cB = cC;
-            cC = cD;
-            cD = sm.next;
-            e0D = e0N;
-            e1D = e1N;
-            sc ^= 1u;
-        } else if constexpr (PF) {
+        if constexpr (PF) {
             cB = cC;
             cC = sm.next;
         } else {
             cB = sm.next;
         }
-    }
-}
-
-// k_lcopy: no active digit after digit 0 (the local pass's logical order is the sorted
-// array): workgroup k gathers logical tile k from TMP into OUT.  Every other sort exits.
-__global__ __launch_bounds__(OSP_BLOCK) void k_lcopy(Bufs b, const Plan *__restrict__ plan, GthTables tb, uint32_t n) {
-    if (plan->copy_from != SEL_TMP) return;
-    __shared__ GthS G;
-    constexpr int KPT = OSP_KPT;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t L0 = blockIdx.x * (uint32_t)OSP_TILE, nv = n - L0 < (uint32_t)OSP_TILE ? n - L0 : (uint32_t)OSP_TILE;
-    uint32_t e0, e1, a, bb, s;
-    gth_range(tb, L0, e0, e1);
-    gth_run(tb, e0, e1, tid, a, bb, s);
-    if (tid < (uint32_t)(OSP_TILE / 64)) G.mask[tid] = 0ull;
-    if (tid == 0) {
-        G.over = e1 - e0 >= (uint32_t)GTH_KMAX;
-        G.e0 = e0;
-        G.e1 = e1;
-    }
-    __syncthreads();
-    gth_mark(G, a, bb, L0, nv);
-    __syncthreads();
-    if (wid == 0) gth_prefix(G, lane);
-    __syncthreads();
-    gth_delta(G, a, bb, s, L0, nv);
-    __syncthreads();
-    uint32_t k[KPT];
-    gth_load<KPT>(G, tb, osp_rsrc(b.p[SEL_TMP], n), L0, nv, wid, lane, 0u, 0, k);
-    const __amdgpu_buffer_rsrc_t rout = osp_rsrc(b.p[SEL_OUT], n);
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-        const uint32_t p = (wid * KPT + (uint32_t)j) * 64u + lane;
-        if (p < nv) __builtin_amdgcn_raw_buffer_store_b32(k[j], rout, (L0 + p) * 4u, 0, 0);
     }
 }
 
@@ -2295,42 +1979,17 @@ static int cu_count() {
 }
 
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
-                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s, const Bufs *vb,
-                             const GthTables *tb) {
+                             uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s, const Bufs *vb) {
     const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE + NSEG;
     const size_t want = (size_t)cu_count();  // one workgroup per CU (LDS-bound)
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);
     if (vb)
-        k_onesweep_p<true><<<g, OSP_KV_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, *vb,
-                                                     GthTables{});
-    else if (tb)
-        k_onesweep_p<false, true><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err,
-                                                          b, *tb);
+        k_onesweep_p<true><<<g, OSP_KV_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, *vb);
     else
-        k_onesweep_p<false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b,
-                                                    GthTables{});
+        k_onesweep_p<false><<<g, OSP_BLOCK, 0, s>>>(b, plan, pass, (uint32_t)n, flip, sp, lookback, counter, err, b);
     return hipGetLastError();
 }
 
-hipError_t launch_plan_l(const uint32_t *tot0, const uint32_t *joint, size_t n, Plan *plan, SegPlan *segplans,
-                         uint32_t *hist, void *zero_p, size_t zero_bytes, hipStream_t s) {
-    // the look-back clear rides in the plan launch (workgroups 1..)
-    const bool fold = zero_bytes % 16 == 0;
-    if (!fold && zero_bytes) {
-        const hipError_t z = launch_zero(zero_p, zero_bytes, s);
-        if (z != hipSuccess) return z;
-    }
-    const size_t zn4 = fold ? zero_bytes / 16 : 0;
-    const unsigned g = 1u + (zn4 ? blocks_for(zn4, 256 * 4, 2048) : 0u);
-    k_plan_l<<<g, 256, 0, s>>>(tot0, joint, (uint32_t)n, plan, segplans, hist, static_cast<uint4 *>(zero_p), zn4);
-    return hipGetLastError();
-}
-
-hipError_t launch_lcopy(Bufs b, const Plan *plan, GthTables tb, size_t n, hipStream_t s) {
-    const unsigned g = (unsigned)((n + OSP_TILE - 1) / OSP_TILE);
-    k_lcopy<<<g, OSP_BLOCK, 0, s>>>(b, plan, tb, (uint32_t)n);
-    return hipGetLastError();
-}
 
 hipError_t launch_hist_seg(const uint32_t *keys, size_t n, uint32_t flip, uint32_t *hps, uint32_t *joint,
                            hipStream_t s) {

@@ -91,13 +91,12 @@ def test_sizes_and_limits(ls):
         assert ls.workspace_bytes(n, "auto") == ls.workspace_bytes(n, "merge")
     for n in ((1 << 16) + 1, 1 << 17, 1 << 18, 1 << 20, 1 << 22, 1 << 28, (1 << 30) - 1):
         assert ls.workspace_bytes(n, "auto") == ls.workspace_bytes(n, "radix")
-    # radix is sized for the implementation that runs: at 2^28 the local-pass
-    # path's two key buffers, 3 launches of look-back words (one slot of 256 digits per
-    # 16384-key tile), the tile rows and the run tables; at 2^20 the gathered passes' two
-    # key buffers and run tables
+    # radix is sized for the implementation that runs: at 2^28 the onesweep
+    # passes' ping-pong keys + 4 passes of look-back words (one slot of 256 digits per
+    # 16384-key tile); at 2^20 the gathered passes' two key buffers and run tables
     n = 1 << 28
     w = ls.workspace_bytes(n, "radix")
-    assert w >= 8 * n + 3 * (n // 16384) * 256 * 4 + 3 * (n // 16384) * 256 * 4 and w < 8 * n + (160 << 20)
+    assert w >= 4 * n + 4 * (n // 16384) * 256 * 4 and w < 4 * n + (128 << 20)
     assert ls.workspace_bytes(1 << 20, "radix") >= 8 * (1 << 20)
 
 
