@@ -1214,352 +1214,6 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
     }
 }
 
-// Keys-only tile sort, persistent and pipelined (merge sort stage 1, the tile-sort small
-// path).  The non-persistent k_tile_sort above holds one 32768-key tile per CU (146 KB of
-// LDS): a workgroup's load waits for nothing else to do, and its four LDS passes leave
-// the memory idle.  Here one 512-thread workgroup per CU (8 wave64s, 64 keys per lane,
-// two waves per SIMD: room for 256 VGPRs) loops over the tiles, the next tile's keys
-// loading into registers while the current one is ranked and reordered in LDS, so each
-// CU's HBM traffic overlaps its LDS work.  Same passes, ranks and uniform-digit skip.
-constexpr int TSP_BLOCK = 512, TSP_KPT = 64;
-static_assert(TSP_BLOCK * TSP_KPT == TS_TILE, "one tile per workgroup iteration");
-struct TspSmem {
-    uint32_t keys[TS_TILE];
-    uint32_t whist[(TSP_BLOCK / WAVE) * 256];
-    uint32_t wsum[8];
-    uint32_t red_and[TSP_BLOCK / WAVE];
-    uint32_t red_or[TSP_BLOCK / WAVE];
-    uint32_t probe[WAVE];
-    uint32_t ordered;
-};
-__global__ __launch_bounds__(TSP_BLOCK, 2) void k_tile_sort_p(const uint32_t *in, uint32_t *out, uint32_t n,
-                                                             uint32_t flip) {
-    constexpr int KPT = TSP_KPT, W = TSP_BLOCK / WAVE, R = 256, TILE = TS_TILE;
-    __shared__ TspSmem sm;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t sentinel = ~0u;  // keys ^ flip in registers
-    const uint32_t ntiles = (n + (uint32_t)TILE - 1u) / (uint32_t)TILE;
-    if (wid == 0) {  // lane-ordered LDS atomics (see k_onesweep_p): rank by one atomic per key
-        const bool ord = lds_lane_ordered(sm.probe, lane);
-        if (lane == 0) sm.ordered = ord ? 1u : 0u;
-    }
-    const __amdgpu_buffer_rsrc_t rin = osp_rsrc(in, n), rout = osp_rsrc(out, n);
-    const uint32_t woff = wid * (KPT * WAVE) + lane;
-    // slot j of a lane at byte offset o + j * 256: as 4 base offsets (one per 16 slots) and
-    // immediate offsets below 4 KiB, so no slot needs an address register of its own
-    auto load = [&](uint32_t t, uint32_t (&k)[KPT]) {  // past n: the sentinel (digit 255)
-        const uint32_t o = (t * (uint32_t)TILE + woff) * 4u;
-        const uint32_t nv = n - t * (uint32_t)TILE;
-#pragma unroll
-        for (int q = 0; q < KPT / 16; ++q) {
-            const uint32_t oq = o + (uint32_t)q * 16u * WAVE * 4u;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int j = q * 16 + i;
-                const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rin, oq, i * WAVE * 4, 0);
-                k[j] = woff + j * WAVE < nv ? v ^ flip : sentinel;
-            }
-        }
-    };
-    uint32_t k[KPT], kn[KPT];
-    uint32_t t = blockIdx.x;
-    if (t < ntiles) load(t, kn);
-    __syncthreads();
-    const bool atomic_rank = __builtin_amdgcn_readfirstlane(sm.ordered) != 0u;
-    uint32_t *wh = sm.whist + wid * R;
-    for (; t < ntiles; t += gridDim.x) {
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = kn[j];
-        if (t + gridDim.x < ntiles) load(t + gridDim.x, kn);
-        const uint32_t nv = n - t * (uint32_t)TILE;
-        // bits on which the tile's keys differ -> passes that are not the identity
-        uint32_t a = ~0u, o = 0u;
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const bool ok = woff + j * WAVE < nv;
-            const uint32_t x = k[j];
-            a &= ok ? x : ~0u;
-            o |= ok ? x : 0u;
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) {
-            a &= __shfl_xor(a, off);
-            o |= __shfl_xor(o, off);
-        }
-        if (lane == 0) {
-            sm.red_and[wid] = a;
-            sm.red_or[wid] = o;
-        }
-        __syncthreads();
-        uint32_t diff;
-        {
-            uint32_t aa = ~0u, oo = 0u;
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                aa &= sm.red_and[w];
-                oo |= sm.red_or[w];
-            }
-            diff = aa ^ oo;
-        }
-        for (int pass = 0; pass < 4; ++pass) {
-            const uint32_t shift = pass * 8;
-            if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the tile
-            for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
-            uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                // (16 returning atomics in flight at most: the scheduler would otherwise
-                // hoist all 64 and their results and addresses out of the 256 VGPRs)
-                if (j % 16 == 0) __builtin_amdgcn_sched_barrier(0);
-                const uint32_t d = (k[j] >> shift) & 0xFFu;
-                uint32_t r;
-                if (atomic_rank) {
-                    r = wave_atomic_rank(wh, d, lane);
-                } else {
-                    const uint64_t m = match8(d);
-                    const uint32_t pre = mbcnt64(m);
-                    const uint32_t old = wh[d];
-                    if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
-                    r = old + pre;
-                }
-                rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
-            }
-            __syncthreads();
-            uint32_t tot = 0;
-            if (tid < (uint32_t)R) {
-#pragma unroll
-                for (int w = 0; w < W; ++w) tot += sm.whist[w * R + tid];
-            }
-            const uint32_t ds = block_excl_scan<TSP_BLOCK, R>(tot, sm.wsum);
-            if (tid < (uint32_t)R) {
-                uint32_t run = ds;
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    const uint32_t c = sm.whist[w * R + tid];
-                    sm.whist[w * R + tid] = run;
-                    run += c;
-                }
-            }
-            __syncthreads();
-            uint32_t sh2 = shift;
-            asm volatile("" : "+s"(sh2));  // recompute the digits (see k_tile_sort3)
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                if (j % 16 == 0) __builtin_amdgcn_sched_barrier(0);
-                const uint32_t d = (k[j] >> sh2) & 0xFFu;
-                sm.keys[wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = k[j];
-            }
-            __syncthreads();
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                if (j % 16 == 0) __builtin_amdgcn_sched_barrier(0);
-                k[j] = sm.keys[woff + j * WAVE];
-            }
-        }
-        const uint32_t o4 = (t * (uint32_t)TILE + woff) * 4u;
-#pragma unroll
-        for (int q = 0; q < KPT / 16; ++q) {
-            const uint32_t oq = o4 + (uint32_t)q * 16u * WAVE * 4u;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int j = q * 16 + i;
-                if (woff + j * WAVE < nv) __builtin_amdgcn_raw_buffer_store_b32(k[j] ^ flip, rout, oq, i * WAVE * 4, 0);
-            }
-        }
-        __syncthreads();  // every wave has read this tile (LDS keys, red_*) before the next one's writes
-    }
-}
-
-// Keys-only tile sort in three LDS passes of 11, 11 and 10 bits instead of four of 8.
-// Every pass costs three LDS accesses per key at random banks (the rank atomic, the
-// wave-offset read and the reorder store; r26: 57 % of the LDS cycles are their bank
-// conflicts), so a pass fewer removes a quarter of them.  2048 counters per wave need
-// 16-bit counters, two per word (a wave ranks at most 4096 keys; offsets stay below
-// 32768), and 8 waves of 64 keys per lane so that 8 x 4 KB of counters and the
-// 128 KB tile fill the 160 KB of LDS exactly: the scan's and the tile's reductions
-// borrow the key area, free between a pass's read-back and the next reorder.
-constexpr int TS3_BLOCK = 512, TS3_KPT = 64, TS3_W = TS3_BLOCK / WAVE, TS3_WORDS = 1024;
-static_assert(TS3_BLOCK * TS3_KPT == TS_TILE, "one tile per workgroup");
-struct Ts3Smem {
-    uint32_t keys[TS_TILE];
-    uint32_t cnt[TS3_W * TS3_WORDS];  // wave w: 2048 16-bit counters, digit d in half d & 1 of word d >> 1
-};
-static_assert(sizeof(Ts3Smem) <= 163840, "fits the CU's LDS");
-
-// Stable rank of digit d (< 2048) among this wave's keys so far on 16-bit counters
-// (see wave_atomic_rank).  Without lane-ordered atomics: peers by ballots, one add per
-// digit by its lowest lane, the old count shuffled to the peers.
-__device__ __forceinline__ uint32_t rank16(uint32_t *cw, uint32_t d, uint32_t lane, bool ordered) {
-    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-    if (__ballot(d != d0) == 0ull) {
-        const uint32_t sh0 = (d0 & 1u) * 16u;
-        uint32_t b = 0;
-        if (lane == 0) b = __hip_atomic_fetch_add(cw + (d0 >> 1), 64u << sh0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        return ((__builtin_amdgcn_readfirstlane(b) >> sh0) & 0xFFFFu) + lane;
-    }
-    const uint32_t sh = (d & 1u) * 16u;
-    if (ordered)
-        return (__hip_atomic_fetch_add(cw + (d >> 1), 1u << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) >> sh) & 0xFFFFu;
-    const uint64_t m = match_digit<11>(d);
-    const uint32_t pre = mbcnt64(m);
-    uint32_t old = 0;
-    if (pre == 0)
-        old = __hip_atomic_fetch_add(cw + (d >> 1), (uint32_t)__popcll(m) << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-    old = (uint32_t)__shfl((int)old, (int)__builtin_ctzll(m));
-    return ((old >> sh) & 0xFFFFu) + pre;
-}
-
-// PERSIST: one workgroup per CU loops over the tiles, the next tile's keys loading into
-// registers (64 more VGPRs) while the current one is sorted in LDS.
-template <bool PERSIST>
-__global__ __launch_bounds__(TS3_BLOCK, 2) void k_tile_sort3(const uint32_t *in, uint32_t *out, uint32_t n, uint32_t flip) {
-    constexpr int KPT = TS3_KPT, W = TS3_W, TILE = TS_TILE;
-    __shared__ Ts3Smem sm;
-    const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-    const uint32_t ntiles = (n + (uint32_t)TILE - 1u) / (uint32_t)TILE;
-    const uint32_t woff = wid * (KPT * WAVE) + lane;
-    uint32_t *scratch = sm.keys;  // [0, 64): lane-order probe; [64, 80): tile and/or; [128, 136): scan
-    if (wid == 0) {
-        const bool ord = lds_lane_ordered(scratch, lane);
-        if (lane == 0) scratch[80] = ord ? 1u : 0u;
-    }
-    // keys ^ flip (unsigned order) from load to store; past n the sentinel, which ranks last
-    auto load = [&](uint32_t t, uint32_t (&k)[KPT]) {
-        const uint32_t base = t * (uint32_t)TILE, nv = n - base < (uint32_t)TILE ? n - base : (uint32_t)TILE;
-        const uint32_t *src = in + base;
-        if (nv == (uint32_t)TILE) {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) k[j] = ld_stream<NT_TILE>(src + woff + j * WAVE) ^ flip;
-        } else {
-#pragma unroll
-            for (int j = 0; j < KPT; ++j) k[j] = woff + j * WAVE < nv ? ld_stream<NT_TILE>(src + woff + j * WAVE) ^ flip : ~0u;
-        }
-    };
-    uint32_t k[KPT], kn[PERSIST ? KPT : 1];
-    uint32_t t = blockIdx.x;
-    if constexpr (PERSIST) {
-        if (t < ntiles) load(t, kn);
-    } else {
-        load(t, k);
-    }
-    __syncthreads();
-    const bool ordered = __builtin_amdgcn_readfirstlane(scratch[80]) != 0u;
-    if (t >= ntiles) return;
-    do {
-    const uint32_t base = t * (uint32_t)TILE;
-    const uint32_t nv = n - base < (uint32_t)TILE ? n - base : (uint32_t)TILE;
-    if constexpr (PERSIST) {
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = kn[j];
-        if (t + gridDim.x < ntiles) load(t + gridDim.x, kn);
-    }
-    uint32_t a = ~0u, o = 0u;
-#pragma unroll
-    for (int j = 0; j < KPT; ++j) {
-        const bool ok = woff + j * WAVE < nv;
-        a &= ok ? k[j] : ~0u;
-        o |= ok ? k[j] : 0u;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        a &= __shfl_xor(a, off);
-        o |= __shfl_xor(o, off);
-    }
-    __syncthreads();  // scratch[64, 80) free: the ordered flag was read, the last tile read back
-    if (lane == 0) {
-        scratch[64 + wid] = a;
-        scratch[72 + wid] = o;
-    }
-    __syncthreads();
-    uint32_t diff;
-    {
-        uint32_t aa = ~0u, oo = 0u;
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-            aa &= scratch[64 + w];
-            oo |= scratch[72 + w];
-        }
-        diff = aa ^ oo;
-    }
-    uint32_t *cw = sm.cnt + wid * TS3_WORDS;
-#pragma unroll 1
-    for (int pass = 0; pass < 3; ++pass) {
-        const uint32_t shift = (uint32_t)pass * 11u;
-        const uint32_t mask = pass == 2 ? 0x3FFu : 0x7FFu;
-        const uint32_t words = pass == 2 ? 512u : 1024u;
-        if (((diff >> shift) & mask) == 0u) continue;  // uniform over the tile
-        __syncthreads();  // the previous pass's read-back (and the reductions) are done with sm.keys
-        for (uint32_t i = lane; i < words; i += WAVE) cw[i] = 0u;
-        uint32_t rank[KPT / 2];
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            if (j % 8 == 0) __builtin_amdgcn_sched_barrier(0);
-            const uint32_t r = rank16(cw, (k[j] >> shift) & mask, lane, ordered);
-            rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
-        }
-        __syncthreads();  // (1) every wave's counts
-        // thread t owns words t (and t + 512): digit totals over the waves, one scan over
-        // the block, then each wave's packed offsets (no carries: every half < 65536)
-        uint32_t tw[2] = {0u, 0u};
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t i = (uint32_t)q * TS3_BLOCK + tid;
-            if (i < words) {
-#pragma unroll
-                for (int w = 0; w < W; ++w) tw[q] += sm.cnt[w * TS3_WORDS + i];
-            }
-        }
-        // digit order is word order, so thread t's words t and t + 512 sit in the two
-        // halves of the digit range: both halves scanned at once as 16-bit fields of one
-        // word (each sum <= 32768); e >> 16 is then relative to the first half's total
-        const uint32_t s0 = (tw[0] & 0xFFFFu) + (tw[0] >> 16), s1 = (tw[1] & 0xFFFFu) + (tw[1] >> 16);
-        const uint32_t e = block_excl_scan<TS3_BLOCK, TS3_BLOCK>(s0 | (s1 << 16), scratch + 128);
-        uint32_t first_total = 0;
-#pragma unroll
-        for (int w = 0; w < W; ++w) first_total += scratch[128 + w] & 0xFFFFu;
-        const uint32_t e0 = e & 0xFFFFu, e1 = e >> 16;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const uint32_t i = (uint32_t)q * TS3_BLOCK + tid;
-            if (i < words) {
-                const uint32_t b = q == 0 ? e0 : first_total + e1;
-                uint32_t run = b | ((b + (tw[q] & 0xFFFFu)) << 16);
-#pragma unroll
-                for (int w = 0; w < W; ++w) {
-                    const uint32_t c = sm.cnt[w * TS3_WORDS + i];
-                    sm.cnt[w * TS3_WORDS + i] = run;
-                    run += c;
-                }
-            }
-        }
-        __syncthreads();  // (2) offsets
-        // the digits again, through an opaque copy of the shift: the compiler would
-        // otherwise keep the rank loop's 64 digits and counter addresses live to here
-        uint32_t sh2 = shift, mk2 = mask;
-        asm volatile("" : "+s"(sh2), "+s"(mk2));
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            if (j % 8 == 0) __builtin_amdgcn_sched_barrier(0);
-            const uint32_t d = (k[j] >> sh2) & mk2;
-            const uint32_t off = (cw[d >> 1] >> ((d & 1u) * 16u)) & 0xFFFFu;
-            sm.keys[off + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu)] = k[j];
-        }
-        __syncthreads();  // (3) the tile in this pass's order
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) k[j] = sm.keys[woff + j * WAVE];
-    }
-    uint32_t *dst = out + base;
-    if (nv == (uint32_t)TILE) {
-#pragma unroll
-        for (int j = 0; j < KPT; ++j) dst[woff + j * WAVE] = k[j] ^ flip;
-    } else {
-#pragma unroll
-        for (int j = 0; j < KPT; ++j)
-            if (woff + j * WAVE < nv) dst[woff + j * WAVE] = k[j] ^ flip;
-    }
-    } while (PERSIST && (t += gridDim.x) < ntiles);
-}
-
 // ---------------------------------------------------------------------------------
 // 64-key tile bit-split sort (radix_sort_kernel's job on a wave64)
 // ---------------------------------------------------------------------------------
@@ -1678,7 +1332,7 @@ __device__ __forceinline__ PairGeom pair_of(uint32_t o, uint32_t n, uint32_t run
 // separate partition launch), then merges tile after tile, the keys of the next
 // tile loading into registers while the current one is merged in LDS.
 // KV: key/value pairs; each output takes the payload of the key it took (vsrc/vdst).
-template <int BLOCK, int KPT, bool KV = false, int PF = 1>
+template <int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                         uint32_t n, uint32_t run, uint32_t flip, uint32_t ntiles,
                                                         uint32_t m, MgPairs pr, const uint32_t *__restrict__ vsrc = nullptr,
@@ -1751,13 +1405,10 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
             if constexpr (KV) vv[j] = k < q.tot ? vsrc[a] : 0u;
         }
     };
-    uint32_t nx[KPT], nx2[PF > 1 ? KPT : 1];
+    uint32_t nx[KPT];
     uint32_t nv[KV ? KPT : 1];
     Geo cur = geo(t0);
     load(cur, nx, nv);
-    if constexpr (PF > 1) {
-        if (t0 + 1 < t1) load(geo(t0 + 1), nx2, nv);
-    }
     for (uint32_t t = t0; t < t1; ++t) {
         __syncthreads();  // previous tile's merge no longer reads sm.in
 #pragma unroll
@@ -1766,18 +1417,11 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
 #pragma unroll
             for (int j = 0; j < KPT; ++j) sm.vin[tid + (uint32_t)j * BLOCK] = nv[j];
         }
-        // next tile: geometry from the co-ranks, keys into registers (PF = 2: the tile
-        // after it is already in flight, and the one after that is issued now)
+        // next tile: geometry from the co-ranks, keys into registers
         Geo nxt = cur;
         if (t + 1 < t1) {
             nxt = geo(t + 1);
-            if constexpr (PF > 1) {
-#pragma unroll
-                for (int j = 0; j < KPT; ++j) nx[j] = nx2[j];
-                if (t + 2 < t1) load(geo(t + 2), nx2, nv);
-            } else {
-                load(nxt, nx, nv);
-            }
+            load(nxt, nx, nv);
         }
         __syncthreads();  // sm.in holds the current tile
         const uint32_t la = cur.la, lb = cur.tot - cur.la, tot = cur.tot;
@@ -2046,15 +1690,7 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) 
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t nt = (n + TS_TILE - 1) / TS_TILE;
-    const char *e = std::getenv("LABSORT_TS_IMPL");  // (r4 A/B, removed after)
-    if (e && e[0] == 'p')
-        k_tile_sort_p<<<(unsigned)(nt < (size_t)cu_count() ? nt : (size_t)cu_count()), TSP_BLOCK, 0, s>>>(in, out, (uint32_t)n, flip);
-    else if (e && e[0] == '3')
-        k_tile_sort3<false><<<(unsigned)nt, TS3_BLOCK, 0, s>>>(in, out, (uint32_t)n, flip);
-    else if (e && e[0] == 'q')
-        k_tile_sort3<true><<<(unsigned)(nt < (size_t)cu_count() ? nt : (size_t)cu_count()), TS3_BLOCK, 0, s>>>(in, out, (uint32_t)n, flip);
-    else
-        k_tile_sort<TS_BLOCK, TS_KPT><<<(unsigned)nt, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
+    k_tile_sort<TS_BLOCK, TS_KPT><<<(unsigned)nt, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
     return hipGetLastError();
 }
 
@@ -2080,13 +1716,7 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
         k_merge_pass_p<MG_BLOCK, MG_KPT, true>
             <<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr, vin, vout);
     else
-    {
-        static const int mg_pf = [] { const char *e = std::getenv("LABSORT_MG_PF"); return e ? std::atoi(e) : 1; }();  // (r4 A/B, removed after)
-        if (mg_pf == 2)
-            k_merge_pass_p<MG_BLOCK, MG_KPT, false, 2><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr);
-        else
-            k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr);
-    }
+        k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr);
     return hipGetLastError();
 }
 
