@@ -1146,43 +1146,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
         uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
         if (atomic_rank) {
-            // stable wave rank by one lane-ordered returning atomic per key, without a
-            // branch per key: a wave whose 64 keys share the digit (sorted or clustered
-            // input) adds 64 once from lane 0 while lanes 1..63 add 0 to slots of their own,
-            // so all KPT atomics issue back to back and are consumed afterwards
-            // (in chunks of RC: a chunk's results are consumed while the next one's are in
-            // flight, which bounds the live results to 2 RC registers)
-            constexpr int RC = 4;
-            uint32_t ret[2][RC];
-            uint32_t uni = 0;  // (wave-uniform) bit j: slot j's digit is the same in every lane
-            auto issue = [&](int c) {
-#pragma unroll
-                for (int i = 0; i < RC; ++i) {
-                    const int j = c * RC + i;
-                    const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-                    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-                    const bool u = __ballot(d != d0) == 0ull;
-                    uni |= (u ? 1u : 0u) << j;
-                    uint32_t *a = u ? (lane ? sm.dummy + wid * WAVE + lane : wh + d0) : wh + d;
-                    ret[c & 1][i] = __hip_atomic_fetch_add(a, u ? (lane ? 0u : 64u) : 1u, __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_WAVEFRONT);
-                }
-            };
-            auto consume = [&](int c) {
-#pragma unroll
-                for (int i = 0; i < RC; ++i) {
-                    const int j = c * RC + i;
-                    const uint32_t r = ((uni >> j) & 1u) ? __builtin_amdgcn_readfirstlane(ret[c & 1][i]) + lane : ret[c & 1][i];
-                    rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
-                }
-            };
-            issue(0);
-#pragma unroll
-            for (int c = 1; c < KPT / RC; ++c) {
-                issue(c);
-                consume(c - 1);
-            }
-            consume(KPT / RC - 1);
+            wave_rank_atomic<KPT>(k, flip, shift, wh, sm.dummy + wid * WAVE, lane, rank);
         } else {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {  // peers by 8 ballots
