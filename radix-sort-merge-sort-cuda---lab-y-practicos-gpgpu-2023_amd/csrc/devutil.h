@@ -110,49 +110,6 @@ __device__ __forceinline__ uint32_t wave_atomic_rank(uint32_t *wh, uint32_t d, u
     return __hip_atomic_fetch_add(wh + d, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
-// Stable wave ranks of the 8-bit digits (k[j] ^ flip) >> shift of a lane's KPT keys
-// (slot-major order), by one lane-ordered returning LDS atomic per key on the wave's
-// counters wh, packed two 16-bit ranks per register.  No branch per key: a slot whose
-// digit every lane shares (sorted or clustered input) adds 64 once from lane 0 while
-// lanes 1..63 add 0 to their own slots of `dummy` (64 words of the wave), instead of 64
-// adds serialised on one counter.  The atomics issue in chunks of RC, a chunk's results
-// consumed while the next chunk's are in flight (at most 2 RC results live).
-template <int KPT, int RC = 4>
-__device__ __forceinline__ void wave_rank_atomic(const uint32_t (&k)[KPT], uint32_t flip, uint32_t shift, uint32_t *wh,
-                                                 uint32_t *dummy, uint32_t lane, uint32_t (&rank)[KPT / 2]) {
-    static_assert(KPT % RC == 0 && KPT <= 32, "whole chunks; one uniform bit per slot");
-    uint32_t ret[2][RC];
-    uint32_t uni = 0;  // (wave-uniform) bit j: slot j's digit is the same in every lane
-    auto issue = [&](int c) {
-#pragma unroll
-        for (int i = 0; i < RC; ++i) {
-            const int j = c * RC + i;
-            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
-            const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-            const bool u = __ballot(d != d0) == 0ull;
-            uni |= (u ? 1u : 0u) << j;
-            uint32_t *a = u ? (lane ? dummy + lane : wh + d0) : wh + d;
-            ret[c & 1][i] =
-                __hip_atomic_fetch_add(a, u ? (lane ? 0u : 64u) : 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
-        }
-    };
-    auto consume = [&](int c) {
-#pragma unroll
-        for (int i = 0; i < RC; ++i) {
-            const int j = c * RC + i;
-            const uint32_t r = ((uni >> j) & 1u) ? __builtin_amdgcn_readfirstlane(ret[c & 1][i]) + lane : ret[c & 1][i];
-            rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
-        }
-    };
-    issue(0);
-#pragma unroll
-    for (int c = 1; c < KPT / RC; ++c) {
-        issue(c);
-        consume(c - 1);
-    }
-    consume(KPT / RC - 1);
-}
-
 // Exclusive scan over the first R threads of the block (value v in thread tid < R,
 // others pass 0).  Must be called by every thread (contains a barrier when R > 64).
 template <int BLOCK, int R>

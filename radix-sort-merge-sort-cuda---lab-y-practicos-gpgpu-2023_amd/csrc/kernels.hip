@@ -1059,7 +1059,6 @@ struct TsSmem {
     uint32_t keys[TILE];
     uint32_t vals[KV ? TILE : 1];  // key/value: the payload follows its key through every pass
     uint32_t whist[W * R];
-    uint32_t dummy[W * WAVE];  // per wave: the slots lanes 1..63 add 0 to when the wave shares a digit
     uint32_t wsum[W];
     uint32_t red_and[W];
     uint32_t red_or[W];
@@ -1145,19 +1144,21 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
         if (((diff >> shift) & 0xFFu) == 0u) continue;  // uniform over the tile
         for (uint32_t i = lane; i < (uint32_t)R; i += WAVE) wh[i] = 0u;
         uint32_t rank[KPT / 2];  // two 16-bit wave-local ranks per register
-        if (atomic_rank) {
-            wave_rank_atomic<KPT>(k, flip, shift, wh, sm.dummy + wid * WAVE, lane, rank);
-        } else {
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {  // peers by 8 ballots
-                const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+        for (int j = 0; j < KPT; ++j) {
+            // stable wave rank: lane-ordered returning atomic, else peers by 8 ballots
+            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
+            uint32_t r;
+            if (atomic_rank) {
+                r = wave_atomic_rank(wh, d, lane);
+            } else {
                 const uint64_t m = match8(d);
                 const uint32_t pre = mbcnt64(m);
                 const uint32_t old = wh[d];
                 if (pre == 0) wh[d] = old + (uint32_t)__popcll(m);
-                const uint32_t r = old + pre;
-                rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
+                r = old + pre;
             }
+            rank[j / 2] = (j & 1) ? rank[j / 2] | (r << 16) : r;
         }
         __syncthreads();
         // tile-wide digit offsets folded into the per-wave offsets: the reorder then
@@ -1178,13 +1179,9 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
             }
         }
         __syncthreads();
-        // the digits again, through an opaque copy of the shift: the compiler would
-        // otherwise keep the rank loop's KPT digits and counter addresses live to here
-        uint32_t sh2 = shift;
-        asm volatile("" : "+s"(sh2));
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
-            const uint32_t d = ((k[j] ^ flip) >> sh2) & 0xFFu;
+            const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
             const uint32_t dst = wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
             sm.keys[dst] = k[j];
             if constexpr (KV) sm.vals[dst] = v[j];
