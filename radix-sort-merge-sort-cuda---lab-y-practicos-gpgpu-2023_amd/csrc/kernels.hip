@@ -1179,10 +1179,18 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
             }
         }
         __syncthreads();
+        // every destination first (replacing its 16-bit rank: dst < TILE), the stores after:
+        // interleaved, each counter read would wait for the store before it (the compiler
+        // cannot tell the stores from the counters), 32 LDS round trips in a row per wave
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t d = ((k[j] ^ flip) >> shift) & 0xFFu;
             const uint32_t dst = wh[d] + ((rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu);
+            rank[j / 2] = (j & 1) ? (rank[j / 2] & 0xFFFFu) | (dst << 16) : (rank[j / 2] & 0xFFFF0000u) | dst;
+        }
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t dst = (rank[j / 2] >> ((j & 1) * 16)) & 0xFFFFu;
             sm.keys[dst] = k[j];
             if constexpr (KV) sm.vals[dst] = v[j];
         }
@@ -1455,12 +1463,17 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
             cur = nxt;
             continue;
         }
+        uint32_t pv[KV ? KPT : 1];  // key/value: the payloads, all read before any store (as k_tile_sort)
+        if constexpr (KV) {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) pv[j] = sm.vin[from[j]];
+        }
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t idx = tid * KPT + j;
             if (idx < tot) {
                 sm.out[idx + (idx >> 5)] = r[j];
-                if constexpr (KV) sm.vout[idx + (idx >> 5)] = sm.vin[from[j]];
+                if constexpr (KV) sm.vout[idx + (idx >> 5)] = pv[j];
             }
         }
         __syncthreads();
