@@ -144,8 +144,9 @@ int labsort_pairs_workspace_status(const void *d_workspace, size_t n, int algo, 
  * timeline, max over ranks; phases may overlap): 0 H2D (host input), 1 local sort,
  * 2 plan (samples + splitters + cut points, collectives included), 3 exchange, 4 merge,
  * 5 D2H tail after the merge (host output), 6 total (host wall time), 7 the plan's own
- * work (phase 2 minus the time spent inside its collectives), 8 the plan's wait (time
- * inside the collectives: mostly waiting for the slowest rank to arrive) */
+ * work (host clock: from the rank's local sort seen complete to the plan's end, minus
+ * the time spent inside its collectives), 8 the plan's wait (time inside the
+ * collectives: mostly waiting for the slowest rank to arrive) */
 #define LABSORT_MULTI_PHASES 9
 /* Collectives of one schedule call, in order: 0 samples (allgather), 1 piece counts
  * (allgather), 2 buffer growth (allgather; runs only when a range outgrew the pre-sized

@@ -25,6 +25,7 @@ struct HostOps {
     std::vector<uint32_t> S, R, T;
     bool less(uint32_t a, uint32_t b) const { return (a ^ flip) < (b ^ flip); }
     void mark(Mark) {}
+    int wait_sorted() { return LABSORT_OK; }
     int local_sort(const uint32_t *in, uint64_t m, const uint32_t **sorted) {
         S.assign(in, in + m);
         std::sort(S.begin(), S.end(), [this](uint32_t a, uint32_t b) { return less(a, b); });

@@ -49,29 +49,88 @@ struct Splitter {
 inline size_t samples_per_rank(int p) { return (size_t)256 * (size_t)p; }
 inline size_t sample_pos(size_t m, size_t s, size_t k) { return (size_t)((unsigned __int128)k * m / s); }
 
-// p-1 splitters at the quantiles of the pooled samples, in (key, rank, position) order
+// p-1 splitters at the quantiles of the pooled samples, in (key, rank, position) order:
+// splitter j is the pooled sample of index j * N / p (N = samples of the non-empty shards).
 inline std::vector<Splitter> choose_splitters(int p, const uint64_t *m, const uint32_t *samples, size_t s,
                                               uint32_t flip) {
-    std::vector<Splitter> pool;
-    pool.reserve(s * (size_t)p);
+    std::vector<Splitter> spl(p > 1 ? p - 1 : 0);
+    std::vector<int> src;  // ranks that sampled (non-empty shards), ascending
+    bool ascending = true;
     for (int r = 0; r < p; ++r) {
         if (!m[r]) continue;  // an empty shard samples nothing
-        for (size_t k = 0; k < s; ++k) {
-            const uint32_t key = samples[(size_t)r * s + k];
-            pool.push_back({key ^ flip, (uint32_t)r, (uint64_t)sample_pos(m[r], s, k), key});
-        }
+        src.push_back(r);
+        const uint32_t *x = samples + (size_t)r * s;
+        for (size_t k = 1; k < s && ascending; ++k) ascending = (x[k] ^ flip) >= (x[k - 1] ^ flip);
     }
-    // a sorted shard's sample positions ascend, so a stable sort by (key, rank) is
-    // the (key, rank, position) order
-    std::stable_sort(pool.begin(), pool.end(), [](const Splitter &a, const Splitter &b) {
-        return a.ord != b.ord ? a.ord < b.ord : a.rank < b.rank;
-    });
-    std::vector<Splitter> spl(p > 1 ? p - 1 : 0);
-    if (pool.empty()) {
+    const size_t N = s * src.size();
+    if (!N) {
         for (auto &x : spl) x = {0u, 0u, 0u, 0u};
         return spl;
     }
-    for (int j = 1; j < p; ++j) spl[j - 1] = pool[(size_t)j * pool.size() / p];
+    auto make = [&](int r, size_t k) {
+        const uint32_t key = samples[(size_t)r * s + k];
+        return Splitter{key ^ flip, (uint32_t)r, (uint64_t)sample_pos(m[r], s, k), key};
+    };
+    if (!ascending) {  // samples of a shard that was not sorted: order the pool outright
+        std::vector<Splitter> pool;
+        pool.reserve(N);
+        for (int r : src)
+            for (size_t k = 0; k < s; ++k) pool.push_back(make(r, k));
+        // sample positions ascend within a rank, so a stable sort by (key, rank) is the
+        // (key, rank, position) order
+        std::stable_sort(pool.begin(), pool.end(), [](const Splitter &a, const Splitter &b) {
+            return a.ord != b.ord ? a.ord < b.ord : a.rank < b.rank;
+        });
+        for (int j = 1; j < p; ++j) spl[j - 1] = pool[(size_t)j * N / p];
+        return spl;
+    }
+    // Sorted shards (the schedule's case): each rank's samples are one ascending run, so
+    // the pooled sample of index t is found without forming the pool -- the smallest key X
+    // with more than t samples <= X (a binary search over the 32-bit key order, counting
+    // by one bound search per run), then among the samples equal to X, taken in (rank,
+    // position) order, the (t - #samples < X)-th.  O(p log s) per key step, no allocation:
+    // at p = 8 (16 Ki samples) a few tens of microseconds on every rank instead of the
+    // ~1 ms a sort of the pool takes.
+    auto count = [&](uint32_t ord, bool le) {  // samples with key < ord (le: <= ord)
+        size_t c = 0;
+        for (int r : src) {
+            const uint32_t *x = samples + (size_t)r * s;
+            size_t lo = 0, hi = s;
+            while (lo < hi) {
+                const size_t mid = (lo + hi) / 2;
+                const uint32_t v = x[mid] ^ flip;
+                if (v < ord || (le && v == ord)) lo = mid + 1;
+                else hi = mid;
+            }
+            c += lo;
+        }
+        return c;
+    };
+    for (int j = 1; j < p; ++j) {
+        const size_t t = (size_t)j * N / p;
+        uint64_t lo = 0, hi = 0xFFFFFFFFull;  // smallest ord in [lo, hi] with count(<= ord) > t
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (count((uint32_t)mid, true) > t) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint32_t X = (uint32_t)lo;
+        size_t rem = t - count(X, false);
+        for (int r : src) {
+            const uint32_t *x = samples + (size_t)r * s;
+            const size_t b = (size_t)(std::lower_bound(x, x + s, X, [&](uint32_t a, uint32_t v) {
+                                          return (a ^ flip) < v;
+                                      }) - x);
+            const size_t e = (size_t)(std::upper_bound(x + b, x + s, X, [&](uint32_t v, uint32_t a) {
+                                          return v < (a ^ flip);
+                                      }) - x);
+            if (rem < e - b) {
+                spl[j - 1] = make(r, b + rem);
+                break;
+            }
+            rem -= e - b;
+        }
+    }
     return spl;
 }
 
@@ -120,6 +179,12 @@ struct Result {
     // when it did not run).  leave - arrive = time spent waiting for the slowest peer
     // (plus the collective's own latency); the rest of the plan phase is this rank's work.
     double arrive[C_NCOLL] = {-1.0, -1.0, -1.0}, leave[C_NCOLL] = {-1.0, -1.0, -1.0};
+    // host wall clock, ms since the call started: the plan phase as this rank's host sees
+    // it, from its local sort observed complete (wait_sorted) to the plan's end.  Its work
+    // = this span minus the time inside the collectives, on one clock (a device-event span
+    // would also count marker packets queued behind other ranks' work when several ranks
+    // share one GPU's hardware queues).
+    double plan_host[2] = {-1.0, -1.0};
     int failed_rank = -1;  // the lowest rank that reported a failure (-1: none)
 };
 
@@ -158,6 +223,7 @@ inline uint64_t recv_estimate(uint64_t total, int p) {
 //     int merge(const uint32_t *recv, const uint64_t *offs, int p, uint32_t *h_sink,
 //               const uint32_t **result)   -- h_sink: also copy the result to this host address
 //     void mark(Mark)
+//     int wait_sorted()   -- blocks until the local sort has completed
 //   Comm (the ranks' communicator):
 //     int size(), rank()
 //     int allgather(const void *h_in, void *h_out, size_t bytes)                      (blocking)
@@ -200,6 +266,8 @@ int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t fli
     int st = injected_failure("local_sort", r);
     if (!st) st = ops.local_sort(in, m, &S);
     ops.mark(M_SORTED);
+    if (!st) st = ops.wait_sorted();
+    res.plan_host[0] = now_ms();
     // 2. status, shard size and samples of every rank
     const size_t s = samples_per_rank(p), rec = 16 + 4 * s;
     std::vector<uint8_t> mine(rec, 0), all(rec * (size_t)p, 0);
@@ -268,6 +336,7 @@ int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t fli
         return st;  // (cannot allocate: total <= est was allocated above)
     }
     ops.mark(M_PLANNED);
+    res.plan_host[1] = now_ms();
     std::vector<const uint32_t *> sp(p, nullptr);
     std::vector<uint32_t *> rp(p, nullptr);
     std::vector<uint64_t> scount(p, 0), rcount(p, 0);

@@ -122,11 +122,29 @@ enum { EV_H2D = dist::M_NMARKS, EV_D2H, EV_NEV };
 struct RankState {
     int dev = -1;
     hipStream_t own = nullptr, copy = nullptr;  // own compute stream (in-process ranks), copy stream
+    // the plan's small launches (samples, bounds), at the highest stream priority: the
+    // runtime gives each priority its own hardware queues, so when several ranks share a
+    // GPU they do not wait in a queue behind another rank's queued sort or merge kernels
+    hipStream_t plan = nullptr;
     hipEvent_t chunk_ev[RANK_CHUNKS] = {}, range_ev[RANK_RANGES] = {};
     hipEvent_t tev[EV_NEV] = {};  // timing: schedule marks, end of H2D, end of D2H
     Buf x, y, ws, mws, recv, out, small, part, errs;
     int nerrs = 0;
+    uint32_t *pin = nullptr;  // pinned host staging of the plan's small copies (samples, bounds)
+    size_t pin_words = 0;
 };
+
+// the rank's pinned staging, at least `words` long (DMA copies instead of pageable staging)
+int grow_pin(RankState &R, size_t words) {
+    if (R.pin && R.pin_words >= words) return LABSORT_OK;
+    if (R.pin) MHIP(hipHostFree(R.pin));
+    R.pin = nullptr;
+    R.pin_words = 0;
+    const size_t want = std::max(words, (size_t)4096);
+    MHIP(hipHostMalloc(reinterpret_cast<void **>(&R.pin), want * 4, hipHostMallocDefault));
+    R.pin_words = want;
+    return LABSORT_OK;
+}
 
 int bind_rank(RankState &R, int dev) {
     if (R.dev == dev && R.own) return LABSORT_OK;
@@ -134,7 +152,7 @@ int bind_rank(RankState &R, int dev) {
         MHIP(hipSetDevice(R.dev));
         for (Buf *b : {&R.x, &R.y, &R.ws, &R.mws, &R.recv, &R.out, &R.small, &R.part, &R.errs})
             if (b->p) MHIP(hipFree(b->p));
-        for (hipStream_t s : {R.own, R.copy})
+        for (hipStream_t s : {R.own, R.copy, R.plan})
             if (s) MHIP(hipStreamDestroy(s));
         for (hipEvent_t e : R.chunk_ev)
             if (e) MHIP(hipEventDestroy(e));
@@ -142,11 +160,15 @@ int bind_rank(RankState &R, int dev) {
             if (e) MHIP(hipEventDestroy(e));
         for (hipEvent_t e : R.tev)
             if (e) MHIP(hipEventDestroy(e));
+        if (R.pin) MHIP(hipHostFree(R.pin));
         R = RankState{};
     }
     MHIP(hipSetDevice(dev));
     MHIP(hipStreamCreateWithFlags(&R.own, hipStreamNonBlocking));
     MHIP(hipStreamCreateWithFlags(&R.copy, hipStreamNonBlocking));
+    int least = 0, greatest = 0;
+    MHIP(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    MHIP(hipStreamCreateWithPriority(&R.plan, hipStreamNonBlocking, greatest));
     for (hipEvent_t &e : R.chunk_ev) MHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t &e : R.range_ev) MHIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     for (hipEvent_t &e : R.tev) MHIP(hipEventCreate(&e));
@@ -164,6 +186,10 @@ struct HipRankOps {
     uint32_t flip() const { return key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u; }
 
     void mark(dist::Mark k) { (void)hipEventRecord(R.tev[k], s); }
+    int wait_sorted() {
+        MHIP(hipEventSynchronize(R.tev[dist::M_SORTED]));
+        return LABSORT_OK;
+    }
 
     // sort one piece in -> out (device) with the workspace; its radix error word copied aside
     int sort_piece(const uint32_t *in, uint32_t *out, size_t len) {
@@ -227,10 +253,13 @@ struct HipRankOps {
     int sample(const uint32_t *S, uint64_t m, size_t n, uint32_t *h_out) {
         int st;
         if ((st = grow(R.small, std::max(n, (size_t)4096) * 4))) return st;
-        k_sample<<<(unsigned)((n + 255) / 256), 256, 0, s>>>(S, m, (uint32_t)n, as<uint32_t>(R.small));
+        if ((st = grow_pin(R, n))) return st;
+        MHIP(hipStreamWaitEvent(R.plan, R.tev[dist::M_SORTED], 0));  // after the local sort
+        k_sample<<<(unsigned)((n + 255) / 256), 256, 0, R.plan>>>(S, m, (uint32_t)n, as<uint32_t>(R.small));
         MHIP(hipGetLastError());
-        MHIP(hipMemcpyAsync(h_out, R.small.p, n * 4, hipMemcpyDeviceToHost, s));
-        MHIP(hipStreamSynchronize(s));
+        MHIP(hipMemcpyAsync(R.pin, R.small.p, n * 4, hipMemcpyDeviceToHost, R.plan));
+        MHIP(hipStreamSynchronize(R.plan));
+        memcpy(h_out, R.pin, n * 4);
         return LABSORT_OK;
     }
 
@@ -238,11 +267,15 @@ struct HipRankOps {
         int st;
         if (!nv) return LABSORT_OK;
         if ((st = grow(R.small, std::max(2 * nv, (size_t)4096) * 4))) return st;
+        if ((st = grow_pin(R, 2 * nv))) return st;
         uint32_t *d = as<uint32_t>(R.small);
-        MHIP(hipMemcpyAsync(d, h_vals, nv * 4, hipMemcpyHostToDevice, s));
-        LCALL(labsort_upper_bound(S, m, key_type, d, nv, d + nv, s));
-        MHIP(hipMemcpyAsync(h_out, d + nv, nv * 4, hipMemcpyDeviceToHost, s));
-        MHIP(hipStreamSynchronize(s));
+        memcpy(R.pin, h_vals, nv * 4);
+        MHIP(hipStreamWaitEvent(R.plan, R.tev[dist::M_SORTED], 0));  // after the local sort
+        MHIP(hipMemcpyAsync(d, R.pin, nv * 4, hipMemcpyHostToDevice, R.plan));
+        LCALL(labsort_upper_bound(S, m, key_type, d, nv, d + nv, R.plan));
+        MHIP(hipMemcpyAsync(R.pin + nv, d + nv, nv * 4, hipMemcpyDeviceToHost, R.plan));
+        MHIP(hipStreamSynchronize(R.plan));
+        memcpy(h_out, R.pin + nv, nv * 4);
         return LABSORT_OK;
     }
 
@@ -343,7 +376,8 @@ struct HipRankOps {
         for (int k = 0; k < dist::C_NCOLL; ++k)
             if (res.arrive[k] >= 0.0) wait += res.leave[k] - res.arrive[k];
         ph[8] = wait;
-        ph[7] = ph[2] > wait ? ph[2] - wait : 0.0;
+        const double span = res.plan_host[1] - res.plan_host[0];  // host clock, as the waits
+        ph[7] = span > wait ? span - wait : 0.0;
     }
 };
 
@@ -871,11 +905,12 @@ int labsort_comm_destroy(labsort_comm_t c) {
         for (Buf *b : {&c->R.x, &c->R.y, &c->R.ws, &c->R.mws, &c->R.recv, &c->R.out, &c->R.small, &c->R.part,
                        &c->R.errs, &c->stage})
             if (b->p) (void)hipFree(b->p);
-        for (hipStream_t s : {c->R.own, c->R.copy})
+        for (hipStream_t s : {c->R.own, c->R.copy, c->R.plan})
             if (s) (void)hipStreamDestroy(s);
         for (hipEvent_t e : c->R.chunk_ev) (void)hipEventDestroy(e);
         for (hipEvent_t e : c->R.range_ev) (void)hipEventDestroy(e);
         for (hipEvent_t e : c->R.tev) (void)hipEventDestroy(e);
+        if (c->R.pin) (void)hipHostFree(c->R.pin);
     }
     delete c;
     return st;
