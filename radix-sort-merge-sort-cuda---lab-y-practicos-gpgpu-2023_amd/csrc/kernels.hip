@@ -1204,8 +1204,25 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
         // (the next pass's reorder writes sm.keys two barriers later)
     }
     if (full) {
+#if defined(TSX_ST)
+        if (!KV && diff != 0u && (((uintptr_t)out) & 15u) == 0) {
+            // the sorted tile (in sm.keys once any pass ran) as lane-contiguous 16-B
+            // nontemporal stores
+            const u32x4 *s4 = reinterpret_cast<const u32x4 *>(sm.keys);
+            u32x4 *o4 = reinterpret_cast<u32x4 *>(out + base);
+#pragma unroll
+            for (int j = 0; j < KPT / 4; ++j) __builtin_nontemporal_store(s4[tid + (uint32_t)j * BLOCK], o4 + tid + (uint32_t)j * BLOCK);
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
+        }
+#elif defined(TSX_NT)
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) __builtin_nontemporal_store(k[j], out + wbase + j * WAVE);
+#else
 #pragma unroll
         for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
+#endif
     } else {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
@@ -1455,11 +1472,26 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
             }
         }
         if (!KV && KPT % 4 == 0 && tot == T && (((uintptr_t)dst) & 15u) == 0) {
-            // a full tile: each thread's KPT outputs are consecutive, so they go straight
-            // to HBM as KPT/4 16-B stores (no LDS staging round trip, one barrier fewer)
-            uint4 *o4 = reinterpret_cast<uint4 *>(dst + cur.o0 + tid * KPT);
+            // a full tile: each thread's KPT outputs are consecutive.  They go to HBM through
+            // a wave-private transpose in sm.out (unused by full tiles): written as each
+            // lane's KPT words, read back lane-contiguous, stored as 16-B nontemporal stores
+            // that each cover 1 KB -- no barrier.  Stored straight from the registers, each
+            // lane's two 16-B stores at a 32-B lane stride leave every wave-store half of
+            // each line: 0.486 ms per pass at 2^28 against 0.464 (r28, harness/exp/r4_mgx.sh).
+            {
+                const uint32_t lane = tid & 63u, w = tid >> 6;
+                uint32_t *wo = sm.out + w * 64u * KPT;
 #pragma unroll
-            for (int j = 0; j < KPT / 4; ++j) o4[j] = make_uint4(r[4 * j], r[4 * j + 1], r[4 * j + 2], r[4 * j + 3]);
+                for (int j = 0; j < KPT / 4; ++j)
+                    *reinterpret_cast<uint4 *>(wo + lane * KPT + 4 * j) =
+                        make_uint4(r[4 * j], r[4 * j + 1], r[4 * j + 2], r[4 * j + 3]);
+                u32x4 *o4 = reinterpret_cast<u32x4 *>(dst + cur.o0 + w * 64u * KPT);
+#pragma unroll
+                for (int j = 0; j < KPT / 4; ++j) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(wo + 4u * (lane + 64u * j));
+                    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, o4 + lane + 64u * j);
+                }
+            }
             cur = nxt;
             continue;
         }
