@@ -1455,34 +1455,48 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
                 vb = bi < lb ? sb[bi] : 0u;
             }
         }
-        if (!KV && KPT % 4 == 0 && tot == T && (((uintptr_t)dst) & 15u) == 0) {
-            // a full tile: each thread's KPT outputs are consecutive.  They go to HBM through
-            // a wave-private transpose in sm.out (unused by full tiles): written as each
-            // lane's KPT words, read back lane-contiguous, stored as 16-B nontemporal stores
-            // that each cover 1 KB -- no barrier.  Stored straight from the registers, each
-            // lane's two 16-B stores at a 32-B lane stride leave every wave-store half of
-            // each line: 0.486 ms per pass at 2^28 against 0.464 (r28, harness/exp/r4_mgx.sh).
-            {
-                const uint32_t lane = tid & 63u, w = tid >> 6;
-                uint32_t *wo = sm.out + w * 64u * KPT;
-#pragma unroll
-                for (int j = 0; j < KPT / 4; ++j)
-                    *reinterpret_cast<uint4 *>(wo + lane * KPT + 4 * j) =
-                        make_uint4(r[4 * j], r[4 * j + 1], r[4 * j + 2], r[4 * j + 3]);
-                u32x4 *o4 = reinterpret_cast<u32x4 *>(dst + cur.o0 + w * 64u * KPT);
-#pragma unroll
-                for (int j = 0; j < KPT / 4; ++j) {
-                    const uint4 v = *reinterpret_cast<const uint4 *>(wo + 4u * (lane + 64u * j));
-                    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, o4 + lane + 64u * j);
-                }
-            }
-            cur = nxt;
-            continue;
-        }
         uint32_t pv[KV ? KPT : 1];  // key/value: the payloads, all read before any store (as k_tile_sort)
         if constexpr (KV) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) pv[j] = sm.vin[from[j]];
+        }
+        if (KPT % 4 == 0 && tot == T && (((uintptr_t)dst) & 15u) == 0 && (!KV || (((uintptr_t)vdst) & 15u) == 0)) {
+            // a full tile: each thread's KPT outputs are consecutive.  They go to HBM through
+            // a wave-private transpose in sm.out (sm.vout for the payloads; both unused by
+            // full tiles): written as each lane's KPT words, read back lane-contiguous,
+            // stored as 16-B nontemporal stores that each cover 1 KB -- no barrier.  Stored
+            // straight from the registers, each lane's two 16-B stores at a 32-B lane stride
+            // leave every wave-store half of each line: 0.486 ms per pass at 2^28 against
+            // 0.464 (r28, harness/exp/r4_mgx.sh).
+            const uint32_t lane = tid & 63u, w = tid >> 6;
+            uint32_t *wo = sm.out + w * 64u * KPT;
+#pragma unroll
+            for (int j = 0; j < KPT / 4; ++j)
+                *reinterpret_cast<uint4 *>(wo + lane * KPT + 4 * j) = make_uint4(r[4 * j], r[4 * j + 1], r[4 * j + 2], r[4 * j + 3]);
+            if constexpr (KV) {
+                uint32_t *wv = sm.vout + w * 64u * KPT;
+#pragma unroll
+                for (int j = 0; j < KPT / 4; ++j)
+                    *reinterpret_cast<uint4 *>(wv + lane * KPT + 4 * j) =
+                        make_uint4(pv[4 * j], pv[4 * j + 1], pv[4 * j + 2], pv[4 * j + 3]);
+            }
+            u32x4 *o4 = reinterpret_cast<u32x4 *>(dst + cur.o0 + w * 64u * KPT);
+#pragma unroll
+            for (int j = 0; j < KPT / 4; ++j) {
+                const uint4 v = *reinterpret_cast<const uint4 *>(wo + 4u * (lane + 64u * j));
+                __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, o4 + lane + 64u * j);
+            }
+            if constexpr (KV) {
+                const uint32_t *wv = sm.vout + w * 64u * KPT;
+                u32x4 *ov4 = reinterpret_cast<u32x4 *>(vdst + cur.o0 + w * 64u * KPT);
+#pragma unroll
+                for (int j = 0; j < KPT / 4; ++j) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(wv + 4u * (lane + 64u * j));
+                    __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, ov4 + lane + 64u * j);
+                }
+            }
+            cur = nxt;
+            continue;
         }
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
