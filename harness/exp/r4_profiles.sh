@@ -5,4 +5,5 @@
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/../.." && pwd)}"
 bash "$R/harness/exp/profile_round.sh" r28 || exit $?
 BENCH_ARGS="--algo merge --no-merge" bash "$R/harness/exp/pmc_kernel.sh" k_tile_sort tile_sort_sq || exit $?
-BENCH_ARGS="--no-merge" bash "$R/harness/exp/pmc_kernel.sh" k_onesweep_p onesweep_sq
+BENCH_ARGS="--no-merge" bash "$R/harness/exp/pmc_kernel.sh" k_onesweep_p onesweep_sq || exit $?
+BENCH_ARGS="--algo merge --no-merge" bash "$R/harness/exp/pmc_kernel.sh" k_merge_pass_p merge_sq
