@@ -29,9 +29,11 @@ constexpr int OSP_KV_BLOCK = 512;  // key/value pass threads (32 pairs each; r26
 constexpr int OSP_LBW = 8;
 // Nontemporal key loads per kernel family (ld_stream in devutil.h).  r19 A/B at 2^28:
 // onesweep passes 0.556 -> 0.523 ms, the upfront histogram ~0.02 ms faster; the tile
-// sort, merge pass and gathered passes were slightly slower with them (not set).
+// sort, merge pass and gathered passes were slightly slower with them (not set).  r28:
+// since the merge pass stores through its transpose, nontemporal loads are faster there,
+// 0.4649 -> 0.4608 ms per pass (alternating runs, profiles/r28_ab_merge_nt_kpt.txt).
 constexpr int NT_OSP = 1, NT_HIST = 2, NT_TILE = 4, NT_MERGE = 8, NT_GS = 16, NT_OS = 32;
-constexpr int NT_LOADS = NT_OSP | NT_HIST;
+constexpr int NT_LOADS = NT_OSP | NT_HIST | NT_MERGE;
 constexpr int OSP_NCTR = 8;  // tile acquisition counters per pass: one per XCD group of segments
 static_assert(OSP_TILE >= OS_TILE, "look-back layout sized by the 1-bit pass tiles");
 
@@ -66,7 +68,9 @@ constexpr int TS_TILE_KV = TS_BLOCK * TS_KPT_KV;
 
 // ---- merge path ----
 // r15 sweep: 512 threads x 8 keys (4096-key tiles), 8 workgroups per CU: 0.488 ms/pass
-// (256 x 8 0.521, 256 x 16 0.553, 1024 x 8 0.510, 4 per CU 0.498-0.627)
+// (256 x 8 0.521, 256 x 16 0.553, 1024 x 8 0.510, 4 per CU 0.498-0.627); r28 with the
+// transposed stores: 512 x 16 0.536-0.539 vs 0.464, 4 / 16 workgroups per CU 0.490 / 0.486
+// vs 0.486, co-rank bracket 1 / 2 / 4 / 16 within 1 % of 8
 constexpr int MG_BLOCK = 512;
 constexpr int MG_KPT = 8;
 constexpr int MG_TILE = MG_BLOCK * MG_KPT;
