@@ -1341,8 +1341,10 @@ __device__ __forceinline__ PairGeom pair_of(uint32_t o, uint32_t n, uint32_t run
 // separate partition launch), then merges tile after tile, the keys of the next
 // tile loading into registers while the current one is merged in LDS.
 // KV: key/value pairs; each output takes the payload of the key it took (vsrc/vdst).
+// Keys only: at most 64 VGPRs (8 waves per SIMD, four 512-thread workgroups per CU: the
+// network merge below needs 71 unbounded, which would leave three).
 template <int BLOCK, int KPT, bool KV = false>
-__global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+__global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                         uint32_t n, uint32_t run, uint32_t flip, uint32_t ntiles,
                                                         uint32_t m, MgPairs pr, const uint32_t *__restrict__ vsrc = nullptr,
                                                         uint32_t *__restrict__ vdst = nullptr) {
@@ -1436,23 +1438,56 @@ __global__ __launch_bounds__(BLOCK) void k_merge_pass_p(const uint32_t *__restri
         const uint32_t la = cur.la, lb = cur.tot - cur.la, tot = cur.tot;
         const uint32_t *sa = sm.in, *sb = sm.in + la;
         const uint32_t d = tid * KPT < tot ? tid * KPT : tot;
-        uint32_t ai = corank(sa, la, sb, lb, d, flip);
-        uint32_t bi = d - ai;
-        uint32_t va = ai < la ? sa[ai] : 0u;
-        uint32_t vb = bi < lb ? sb[bi] : 0u;
         uint32_t r[KPT];
         uint32_t from[KV ? KPT : 1];  // key/value: LDS slot (sm.in) of each output
+        if constexpr (!KV) {
+            // keys only: the thread's KPT outputs are the KPT smallest of A[ai, ai+KPT) and
+            // B[bi, bi+KPT) (equal keys are identical words, so the order among them does not
+            // matter): both windows read at once, merged by a bitonic network in registers
+            // (A ascending, B reversed), instead of KPT dependent LDS reads with a branch
+            // each: 0.458 -> 0.437 ms per pass at 2^28 (r28, profiles/r28_ab_merge_network.txt;
+            // a copy in place of any merge: 0.424)
+            const uint32_t ai = corank(sa, la, sb, lb, d, flip), bi = d - ai;
+            uint32_t x[2 * KPT];
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) {
-            const bool takeA = (bi >= lb) || (ai < la && key_le(va, vb, flip));
-            r[j] = takeA ? va : vb;
-            if constexpr (KV) from[j] = takeA ? ai : la + bi;
-            if (takeA) {
-                ++ai;
-                va = ai < la ? sa[ai] : 0u;
-            } else {
-                ++bi;
-                vb = bi < lb ? sb[bi] : 0u;
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t ia = ai + (uint32_t)j, ib = bi + (uint32_t)j;
+                const uint32_t va = sm.in[min(ia, T - 1u)] ^ flip;       // sa = sm.in
+                const uint32_t vb = sm.in[min(la + ib, T - 1u)] ^ flip;  // sb = sm.in + la
+                x[j] = ia < la ? va : 0xFFFFFFFFu;
+                x[2 * KPT - 1 - j] = ib < lb ? vb : 0xFFFFFFFFu;
+            }
+#pragma unroll
+            for (int s = KPT; s >= 1; s >>= 1) {
+#pragma unroll
+                for (int i = 0; i < 2 * KPT; ++i) {
+                    if ((i & s) == 0) {
+                        const uint32_t lo = min(x[i], x[i + s]), hi = max(x[i], x[i + s]);
+                        x[i] = lo;
+                        x[i + s] = hi;
+                    }
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) r[j] = x[j] ^ flip;
+        } else {
+            // key/value: stable, A before B on equal keys, each output's LDS slot kept
+            uint32_t ai = corank(sa, la, sb, lb, d, flip);
+            uint32_t bi = d - ai;
+            uint32_t va = ai < la ? sa[ai] : 0u;
+            uint32_t vb = bi < lb ? sb[bi] : 0u;
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const bool takeA = (bi >= lb) || (ai < la && key_le(va, vb, flip));
+                r[j] = takeA ? va : vb;
+                if constexpr (KV) from[j] = takeA ? ai : la + bi;
+                if (takeA) {
+                    ++ai;
+                    va = ai < la ? sa[ai] : 0u;
+                } else {
+                    ++bi;
+                    vb = bi < lb ? sb[bi] : 0u;
+                }
             }
         }
         uint32_t pv[KV ? KPT : 1];  // key/value: the payloads, all read before any store (as k_tile_sort)
