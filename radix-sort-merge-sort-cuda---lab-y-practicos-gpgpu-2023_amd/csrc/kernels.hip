@@ -1471,7 +1471,9 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
 #pragma unroll
             for (int j = 0; j < KPT; ++j) r[j] = x[j] ^ flip;
         } else {
-            // key/value: stable, A before B on equal keys, each output's LDS slot kept
+            // key/value: stable, A before B on equal keys, each output's LDS slot kept (the
+            // network on 64-bit (key, slot) words measured equal, 13.87-13.94 vs 13.94-13.96
+            // ms per 2^28-pair merge sort: profiles/r28_ab_kv_network.txt)
             uint32_t ai = corank(sa, la, sb, lb, d, flip);
             uint32_t bi = d - ai;
             uint32_t va = ai < la ? sa[ai] : 0u;
