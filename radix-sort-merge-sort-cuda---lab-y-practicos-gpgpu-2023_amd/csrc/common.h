@@ -70,7 +70,8 @@ constexpr int TS_TILE_KV = TS_BLOCK * TS_KPT_KV;
 // r15 sweep: 512 threads x 8 keys (4096-key tiles), 8 workgroups per CU: 0.488 ms/pass
 // (256 x 8 0.521, 256 x 16 0.553, 1024 x 8 0.510, 4 per CU 0.498-0.627); r28 with the
 // transposed stores: 512 x 16 0.536-0.539 vs 0.464, 4 / 16 workgroups per CU 0.490 / 0.486
-// vs 0.486, co-rank bracket 1 / 2 / 4 / 16 within 1 % of 8
+// vs 0.486, co-rank bracket 1 / 2 / 4 / 16 within 1 % of 8; with the network merge 1024 x 8
+// 0.4404 vs 0.4360 (profiles/r28_ab_merge_block1024.txt)
 constexpr int MG_BLOCK = 512;
 constexpr int MG_KPT = 8;
 constexpr int MG_TILE = MG_BLOCK * MG_KPT;
