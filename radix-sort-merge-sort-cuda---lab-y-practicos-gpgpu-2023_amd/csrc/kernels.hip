@@ -1072,7 +1072,11 @@ struct TsSmem {
 // stable, so equal keys keep their input order and their payloads with them.
 // Measured and not kept (r26): a persistent grid, the next tile's keys
 // loaded before the last pass, 16-B grouped loads and stores; r28: nontemporal output
-// stores (1.10 vs 1.07 ms at 2^28), as 16-B stores read from the sorted LDS tile 1.12.
+// stores (1.10 vs 1.07 ms at 2^28), as 16-B stores read from the sorted LDS tile 1.12;
+// the rank loop's per-key uniform-digit branch makes each pass's 32 returning atomics
+// wait one at a time (lgkmcnt(0) at every join), but a per-wave pre-check that runs them
+// branch-free when no digit is wave-uniform measured 1.085-1.092 vs 1.080-1.083 ms (128
+// VGPRs, 3 spilled; profiles/r28_ab_tile_sort_precheck.txt).
 template <int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint32_t *out, const uint32_t *vin,
                                                          uint32_t *vout, uint32_t n, uint32_t flip) {
