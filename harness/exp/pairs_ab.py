@@ -1,0 +1,52 @@
+"""A/B of the 2^28 key/value radix sort across liblabsort builds (paths on the command
+line, relative to the repo root), alternating, each sort event-timed on the stream, plus
+the per-launch onesweep time from the library's own timing class.  Only C-ABI entry points
+every round's build exports are used (labsort_fill, labsort_sort_pairs_device, timing).
+Usage: python harness/exp/pairs_ab.py LIB_A LIB_B [reps]"""
+import ctypes, json, os, sys
+import torch
+
+R = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+libs = [a for a in sys.argv[1:] if not a.isdigit()]
+reps = int(next((a for a in sys.argv[1:] if a.isdigit()), "3"))
+n = 1 << int(os.environ.get("LOG2N", "28"))
+p, sz = ctypes.c_void_p, ctypes.c_size_t
+L = {}
+for lib in libs:
+    h = ctypes.CDLL(os.path.join(R, lib))
+    h.labsort_fill.argtypes = [p, sz, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, p]
+    h.labsort_pairs_workspace_bytes.argtypes = [sz, ctypes.c_int]
+    h.labsort_pairs_workspace_bytes.restype = sz
+    h.labsort_sort_pairs_device.argtypes = [p, p, p, p, sz, ctypes.c_int, ctypes.c_int, p, sz, p]
+    h.labsort_timing_read.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
+    L[lib] = h
+k = torch.empty(n, dtype=torch.int32, device="cuda")
+v = torch.arange(n, dtype=torch.int32, device="cuda")
+ko, vo = torch.empty_like(k), torch.empty_like(v)
+st = torch.cuda.current_stream().cuda_stream
+first = L[libs[0]]
+assert first.labsort_fill(k.data_ptr(), n, 0x5EED0003, 0, 0, 0, p(st)) == 0
+wsb = max(h.labsort_pairs_workspace_bytes(n, 0) for h in L.values())
+ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+ref = None
+for r in range(reps):
+    for lib, h in L.items():
+        call = lambda: h.labsort_sort_pairs_device(k.data_ptr(), v.data_ptr(), ko.data_ptr(), vo.data_ptr(), n, 0, 0,
+                                                   ws.data_ptr(), wsb, p(st))
+        for _ in range(3):
+            assert call() == 0
+        torch.cuda.synchronize()
+        h.labsort_timing_enable(1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            assert call() == 0
+        e1.record()
+        torch.cuda.synchronize()
+        ms, cnt = ctypes.c_double(), ctypes.c_longlong()
+        h.labsort_timing_read(1, ctypes.byref(ms), ctypes.byref(cnt))
+        h.labsort_timing_enable(0)
+        sig = (int(ko[:: 1 << 12].sum().item()), int(vo[:: 1 << 12].sum().item()))
+        ref = ref or sig
+        print(json.dumps({"lib": lib, "rep": r, "sort_ms": round(e0.elapsed_time(e1) / 10, 4),
+                          "pass_ms": round(ms.value / max(cnt.value, 1), 4), "same_output": sig == ref}), flush=True)

@@ -193,7 +193,17 @@ typedef struct {
                      const size_t *recv_bytes);
 } labsort_host_coll;
 int labsort_comm_unique_id(void *id);
+/* RCCL communicators are nonblocking (ncclConfig_t blocking = 0): every wait on the peers
+ * -- the communicator's creation, each collective, the exchange -- polls
+ * ncclCommGetAsyncError and ends at a deadline (LABSORT_COMM_TIMEOUT_S by default).  A
+ * rank whose peer never arrives (its transport broke, it left) then returns
+ * LABSORT_ERR_PEER and its communicator is aborted (ncclCommAbort: its kernels and proxy
+ * stop); later sorts on an aborted communicator return LABSORT_ERR_PEER at once. */
+#define LABSORT_COMM_TIMEOUT_S 120.0
 int labsort_comm_init_rccl(labsort_comm_t *comm, const void *id, int nranks, int rank);
+/* the deadline of every wait on the peers: of `comm`, or (comm NULL) of the in-process
+ * ranks' RCCL transport and of the communicators created afterwards */
+int labsort_comm_set_timeout(labsort_comm_t comm, double seconds);
 int labsort_comm_init_host(labsort_comm_t *comm, int nranks, int rank, const labsort_host_coll *coll);
 int labsort_comm_destroy(labsort_comm_t comm);
 /* This rank's shard d_keys[0..m) (device, on the comm's device; left untouched) in;
@@ -207,6 +217,13 @@ int labsort_dist_timing(labsort_comm_t comm, double *phase_ms, int nphases, size
 /* this rank's arrival / return times at the collectives of its last sort (ncoll entries) */
 int labsort_dist_collectives(labsort_comm_t comm, double *arrive, double *leave, int ncoll);
 int labsort_dist_last_hip_error(labsort_comm_t comm);
+/* TEST HOOK of the multi-GPU schedule (tests only; the product never arms it): rank
+ * `rank` of the following labsort_dist_sort / labsort_sort_host_ranks calls fails at
+ * `phase` -- "local_sort", "bounds", "recv", "grow" (the receive buffer's growth round) or
+ * "exchange" (it leaves without taking part: a broken transport) -- as an out-of-memory
+ * or an expired device spin would.  phase NULL disarms; an unknown phase is
+ * LABSORT_ERR_ARG.  Process-wide. */
+int labsort_test_fault(const char *phase, int rank);
 
 /* ---- key/value (sort_by_key; no lab.cu counterpart, the reference sorts
  * keys only) ----

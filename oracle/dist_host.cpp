@@ -72,8 +72,9 @@ struct CbComm {
     int p, me;
     int size() const { return p; }
     int rank() const { return me; }
+    // a failed callback: the caller's transport failed or a peer left it (as multi.hip's HostCbComm)
     int allgather(const void *in, void *out, size_t bytes) {
-        return cb.allgather(cb.ctx, in, out, bytes) ? LABSORT_ERR_ARG : LABSORT_OK;
+        return cb.allgather(cb.ctx, in, out, bytes) ? LABSORT_ERR_PEER : LABSORT_OK;
     }
     int exchange(const uint32_t *const *send, const uint64_t *sc, uint32_t *const *recv, const uint64_t *rc) {
         std::vector<size_t> sb(p), rb(p);
@@ -87,7 +88,7 @@ struct CbComm {
         for (int j = 0; j < p; ++j) tr += rb[j] / 4;
         hs.resize(std::max<size_t>(hs.size(), 1));
         hr.resize(std::max<size_t>(tr, 1));
-        if (cb.alltoallv(cb.ctx, hs.data(), sb.data(), hr.data(), rb.data())) return LABSORT_ERR_ARG;
+        if (cb.alltoallv(cb.ctx, hs.data(), sb.data(), hr.data(), rb.data())) return LABSORT_ERR_PEER;
         size_t o = 0;
         for (int j = 0; j < p; ++j) {
             if (rb[j]) memcpy(recv[j], hr.data() + o, rb[j]);
@@ -95,11 +96,21 @@ struct CbComm {
         }
         return LABSORT_OK;
     }
+    void abandon() {}  // the peers' gloo collective ends at the group's timeout
 };
+
+labsort::dist::Fault g_fault;  // armed by oracle_test_fault (tests only)
 
 }  // namespace
 
 extern "C" {
+
+// Arm (phase "local_sort" | "bounds" | "recv" | "grow" | "exchange", rank) or disarm
+// (NULL / unknown phase) the schedule's test failure for the following oracle_dist_sort calls.
+void oracle_test_fault(const char *phase, int rank) {
+    g_fault.phase = labsort::dist::fault_phase(phase);
+    g_fault.rank = g_fault.phase ? rank : -1;
+}
 
 // One rank of the product's distributed sort schedule on host shards.  out: room for
 // `cap` keys; *count = keys of this rank's range, *goff = its global offset.  Returns a
@@ -110,7 +121,7 @@ int oracle_dist_sort(const uint32_t *shard, uint64_t m, int key_type, int world,
     HostOps ops{key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u, {}, {}, {}};
     CbComm comm{*coll, world, rank};
     labsort::dist::Result res;
-    const int st = labsort::dist::sort_rank(ops, comm, shard, m, ops.flip, nullptr, res);
+    const int st = labsort::dist::sort_rank(ops, comm, shard, m, ops.flip, nullptr, res, g_fault);
     if (st) return st;
     *count = res.count;
     *goff = res.goff;

@@ -70,6 +70,8 @@ def lib() -> ctypes.CDLL:
         L.labcu_bsearch.argtypes = [p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.oracle_dist_sort.argtypes = [p, u64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(_HostColl),
                                        p, u64, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+        L.oracle_test_fault.argtypes = [ctypes.c_char_p, ctypes.c_int]
+        L.oracle_test_fault.restype = None
         _lib = L
     return _lib
 
@@ -147,6 +149,12 @@ def time_sort_u32(keys: np.ndarray, threads: int = 1, reps: int = 1) -> float:
     keys = np.ascontiguousarray(keys, dtype=np.uint32)
     scratch = np.empty_like(keys)
     return lib().oracle_time_sort_u32(_ptr(keys), keys.size, threads, reps, _ptr(scratch))
+
+
+def test_fault(phase: str | None, rank: int = -1) -> None:
+    """Arm (phase, rank) -- "local_sort", "bounds", "recv", "grow" or "exchange" -- or
+    disarm (None) the schedule's test failure for the following dist_sort calls."""
+    lib().oracle_test_fault(phase.encode() if phase else None, rank)
 
 
 def dist_sort(shard: np.ndarray, key: str, world: int, rank: int, coll, cap: int = 0) -> tuple[np.ndarray, int]:

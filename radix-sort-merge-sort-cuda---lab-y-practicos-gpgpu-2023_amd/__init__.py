@@ -48,6 +48,7 @@ C_SYMBOLS = [
     "labsort_comm_unique_id", "labsort_comm_init_rccl", "labsort_comm_init_host", "labsort_comm_destroy",
     "labsort_dist_sort", "labsort_dist_timing", "labsort_dist_last_hip_error",
     "labsort_multi_collectives", "labsort_dist_collectives", "labsort_copy",
+    "labsort_comm_set_timeout", "labsort_test_fault",
 ]
 XFER = {"auto": 0, "rccl": 1, "peer": 2}
 MULTI_PHASES = ["h2d", "local_sort", "plan", "exchange", "merge", "d2h", "total", "plan_work", "plan_wait"]
@@ -156,6 +157,8 @@ def _load() -> ctypes.CDLL:
     L.labsort_comm_init_rccl.argtypes = [ctypes.POINTER(p), p, i, i]
     L.labsort_comm_init_host.argtypes = [ctypes.POINTER(p), i, i, ctypes.POINTER(HostColl)]
     L.labsort_comm_destroy.argtypes = [p]
+    L.labsort_comm_set_timeout.argtypes = [p, ctypes.c_double]
+    L.labsort_test_fault.argtypes = [ctypes.c_char_p, i]
     L.labsort_dist_sort.argtypes = [p, p, sz, i, p, ctypes.POINTER(p), ctypes.POINTER(sz), ctypes.POINTER(sz)]
     L.labsort_dist_timing.argtypes = [p, ctypes.POINTER(ctypes.c_double), i, ctypes.POINTER(sz)]
     L.labsort_dist_last_hip_error.argtypes = [p]
@@ -304,6 +307,19 @@ def multi_plan(shards, key: str = "u32") -> np.ndarray:
     return np.array(list(cuts), dtype=np.int64).reshape(p, p + 1)
 
 
+def test_fault(phase: str | None, rank: int = -1) -> None:
+    """TEST HOOK (labsort_test_fault): rank `rank` of the following multi-GPU sorts of this
+    process fails at `phase` ("local_sort", "bounds", "recv", "grow", "exchange"); None
+    disarms.  The product never arms it."""
+    _check(lib.labsort_test_fault(phase.encode() if phase else None, rank), "test_fault")
+
+
+def set_comm_timeout(seconds: float) -> None:
+    """Deadline of every wait on the peers of the in-process RCCL transport and of the
+    communicators created afterwards (labsort_comm_set_timeout(NULL, seconds))."""
+    _check(lib.labsort_comm_set_timeout(None, float(seconds)), "comm_set_timeout")
+
+
 class DistComm:
     """One rank's communicator of the distributed merge sort (labsort_comm_t; one
     process per GPU).  DistComm.rccl(world, rank, uid) over RCCL (uid from
@@ -349,7 +365,8 @@ class DistComm:
         """As sort(), with the range as an int32 torch tensor and its global offset.  By
         default the range is copied out of the communicator's buffer; copy=False returns a
         zero-copy view of that buffer instead, which keeps this communicator alive but is
-        overwritten by its next sort."""
+        INVALID after its next sort: that sort may overwrite the buffer, or free it and
+        allocate a larger one (a range that outgrew it), leaving the view on freed memory."""
         ptr, cnt, goff = self.sort(d_keys, m, key, stream)
         v = self.view(ptr, cnt, owner=self)
         return (v.clone() if copy else v), goff
@@ -371,6 +388,10 @@ class DistComm:
         t = torch.as_tensor(holder, device="cuda")
         t._labsort_owner = holder  # the buffer's owner lives as long as the tensor
         return t
+
+    def set_timeout(self, seconds: float) -> None:
+        """Deadline of this communicator's waits on its peers (RCCL; labsort_comm_set_timeout)."""
+        _check(lib.labsort_comm_set_timeout(self.h, float(seconds)), "comm_set_timeout")
 
     def timing(self) -> tuple[dict, int]:
         ms = (ctypes.c_double * len(MULTI_PHASES))()

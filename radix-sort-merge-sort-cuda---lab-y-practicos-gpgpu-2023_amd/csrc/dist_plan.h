@@ -191,22 +191,33 @@ struct Result {
 // Phase marks the schedule reports to the rank operations (timing hooks)
 enum Mark { M_START = 0, M_SORTED, M_PLANNED, M_EXCHANGED, M_MERGED, M_NMARKS };
 
-// Test hook (LABSORT_TEST_FAIL=<phase>:<rank>, phase local_sort | bounds | recv): the
-// named rank reports a failure at that step, as an out-of-memory or an expired device
-// spin would; the tests check that every rank then returns an error instead of waiting
-// for the failed one.
-inline int injected_failure(const char *phase, int r) {
-    const char *e = getenv("LABSORT_TEST_FAIL");
-    if (!e) return LABSORT_OK;
-    const char *c = strchr(e, ':');
-    if (!c || (size_t)(c - e) != strlen(phase) || strncmp(e, phase, (size_t)(c - e)) != 0) return LABSORT_OK;
-    return atoi(c + 1) == r ? LABSORT_ERR_DEVICE : LABSORT_OK;
+// Test hook: the named rank reports a failure at that step, as an out-of-memory or an
+// expired device spin would (F_EXCHANGE: its transport breaks -- it leaves without taking
+// part in the exchange); the tests check that every rank then returns an error instead of
+// waiting for the failed one.  Armed only through the test entry points
+// (labsort_test_fault, oracle_test_fault): no environment variable is read on a sort.
+enum FaultPhase { F_NONE = 0, F_LOCAL_SORT, F_BOUNDS, F_RECV, F_GROW, F_EXCHANGE, F_NPHASES };
+struct Fault {
+    int phase = F_NONE;
+    int rank = -1;
+};
+// phase name of the test entry points ("local_sort", "bounds", "recv", "grow", "exchange")
+inline int fault_phase(const char *name) {
+    static const char *const names[F_NPHASES] = {"", "local_sort", "bounds", "recv", "grow", "exchange"};
+    for (int i = 1; name && i < F_NPHASES; ++i)
+        if (!strcmp(name, names[i])) return i;
+    return F_NONE;
+}
+inline int injected(const Fault &f, int phase, int r) {
+    return f.phase == phase && f.rank == r ? LABSORT_ERR_DEVICE : LABSORT_OK;
 }
 
-// Receive buffer sized before the counts are known: every range lies within about
-// m / (256 p) keys of n / p (samples_per_rank), so 1.25 n / p (+ 64 Ki keys) covers it
-// unless the communicator is broken; a rank whose range is larger grows its buffer in an
-// extra status round that every rank takes part in (all ranks see all the counts).
+// Receive buffer sized before the counts are known.  With equal shards every range lies
+// within about m / (256 p) keys of n / p (samples_per_rank), so 1.25 n / p (+ 64 Ki keys)
+// covers it.  The samples are not weighted by shard size, so unequal shards can exceed it
+// (shards of 10^6 and 10^3 keys, the small one holding the largest keys: range 0 is the
+// whole big shard); a rank whose range is larger grows its buffer in an extra status
+// round that every rank takes part in (all ranks see all the counts, so all take it).
 inline uint64_t recv_estimate(uint64_t total, int p) {
     const uint64_t share = (total + (uint64_t)p - 1) / (uint64_t)p;
     return share + share / 4 + ((uint64_t)1 << 16);
@@ -228,7 +239,11 @@ inline uint64_t recv_estimate(uint64_t total, int p) {
 //     int size(), rank()
 //     int allgather(const void *h_in, void *h_out, size_t bytes)                      (blocking)
 //     int exchange(const uint32_t *const *send, const uint64_t *scount,
-//                  uint32_t *const *recv, const uint64_t *rcount)   -- self pieces excluded
+//                  uint32_t *const *recv, const uint64_t *rcount)   -- self pieces excluded;
+//                  a peer that never takes part must not block it forever (RCCL: a
+//                  deadline, then ncclCommAbort; host callbacks: the caller's timeout)
+//     void abandon()   -- this rank leaves without taking part in the exchange (its
+//                  transport broke): tell the peers now where the communicator can
 // `h_out_base` (nullable): the caller's host array of the whole sorted output; this
 // rank's range is copied to h_out_base + goff.
 //
@@ -240,7 +255,7 @@ inline uint64_t recv_estimate(uint64_t total, int p) {
 // fails returns that failure at once.
 template <class Ops, class Comm>
 int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t flip, uint32_t *h_out_base,
-              Result &res) {
+              Result &res, const Fault &fault = Fault{}) {
     const int p = comm.size(), r = comm.rank();
     const auto t_start = std::chrono::steady_clock::now();
     auto now_ms = [&]() {
@@ -263,7 +278,7 @@ int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t fli
     };
     ops.mark(M_START);
     const uint32_t *S = nullptr;
-    int st = injected_failure("local_sort", r);
+    int st = injected(fault, F_LOCAL_SORT, r);
     if (!st) st = ops.local_sort(in, m, &S);
     ops.mark(M_SORTED);
     if (!st) st = ops.wait_sorted();
@@ -291,12 +306,12 @@ int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t fli
     const std::vector<uint32_t> vals = plan_values(spl, p, flip);
     std::vector<uint32_t> ub(vals.size(), 0u);
     std::vector<uint64_t> cut(p + 1, 0);
-    if (!st) st = injected_failure("bounds", r);
+    if (!st) st = injected(fault, F_BOUNDS, r);
     if (!st && m) st = ops.bounds(S, m, vals.data(), vals.size(), ub.data());
     if (!st) st = rank_cuts(r, m, spl, ub.data(), p, cut.data());
     const uint64_t est = recv_estimate(ntot, p);
     uint32_t *R = nullptr;
-    if (!st) st = injected_failure("recv", r);
+    if (!st) st = injected(fault, F_RECV, r);
     if (!st) st = ops.recv_buffer(est, &R);
     // 5. status and piece counts of every rank: C[i * p + j] = keys rank i sends to rank j
     std::vector<uint64_t> sc(p, 0), C((size_t)p * p);
@@ -327,7 +342,8 @@ int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t fli
         for (int j = 0; j < r; ++j) goff += C[(size_t)i * p + j];
     const uint64_t total = roff[p];
     if (rmax > est) {  // some range outgrew the pre-sized buffers: grow, then agree again
-        st = ops.recv_buffer(total, &R);
+        st = injected(fault, F_GROW, r);
+        if (!st) st = ops.recv_buffer(total, &R);
         std::vector<uint8_t> gm(8, 0), ga(8 * (size_t)p, 0);
         sw = (uint32_t)st;
         memcpy(gm.data(), &sw, 4);
@@ -348,6 +364,12 @@ int sort_rank(Ops &ops, Comm &comm, const uint32_t *in, uint64_t m, uint32_t fli
         rp[j] = R + roff[j];
         rcount[j] = C[(size_t)j * p + r];
         sent += 4 * sc[j];
+    }
+    // (a rank whose transport breaks here leaves its peers inside the exchange: the
+    // communicators bound that wait -- RCCL by a deadline and ncclCommAbort)
+    if ((st = injected(fault, F_EXCHANGE, r))) {
+        comm.abandon();
+        return st;
     }
     if ((st = comm.exchange(sp.data(), scount.data(), rp.data(), rcount.data()))) return st;
     // (the own piece after the exchange: nothing can fail between the agreement and it)

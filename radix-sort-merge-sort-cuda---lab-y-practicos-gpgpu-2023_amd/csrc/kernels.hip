@@ -669,6 +669,11 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Bufs bufs, const Plan *__res
 // The measured history of this loop (shapes, barriers, prefetch, store widths,
 // acquisition) is in DESIGN.md §3.1; the variants measured slower are gone from here.
 // ---------------------------------------------------------------------------------
+// A buffer descriptor's num_records is a 32-bit byte count: n words fit only while
+// 4 n < 2^32.  The radix passes stop at RADIX_MAX_N (2^30 - 1) keys, which the launcher
+// checks (launch_onesweep_p); any kernel on the merge path (n up to 2^31 - 1) that adopts
+// buffer loads must split its descriptor instead (a 2^30-key merge once read zeros this way).
+static_assert((uint64_t)RADIX_MAX_N * 4u <= 0xFFFFFFFFull, "buffer descriptor byte count wraps");
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t osp_rsrc(const uint32_t *p, uint32_t n) {
     const uint64_t a = (uint64_t)p;  // wave-uniform: readfirstlane lets the compiler prove it
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
@@ -1028,10 +1033,13 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
 #pragma unroll
                 for (int q = 0; q < 4; ++q) kA[4 * g + q] = sm.keys[osp_pad(4u * ((uint32_t)g * BLK + tid) + (uint32_t)q)];
         } else {
+            // keys first, then the payloads (interleaved reads measured 1.6 % slower for the
+            // key/value pass: 0.887 vs 0.873 ms, r29 harness/exp/pairs_ab.py)
 #pragma unroll
-            for (int j = 0; j < KPT; ++j) {
-                kA[j] = sm.keys[osp_pad(j * BLK + tid)];
-                if constexpr (KV) vA[j] = sm.vals[osp_pad(j * BLK + tid)];
+            for (int j = 0; j < KPT; ++j) kA[j] = sm.keys[osp_pad(j * BLK + tid)];
+            if constexpr (KV) {
+#pragma unroll
+                for (int j = 0; j < KPT; ++j) vA[j] = sm.vals[osp_pad(j * BLK + tid)];
             }
         }
         // each wave clears its own counters (no barrier before the next ranking)
@@ -1270,13 +1278,15 @@ __device__ __forceinline__ uint32_t corank(const uint32_t *A, uint32_t la, const
     return lo;
 }
 
+// 16-B aligned: the full-tile path reads and writes sm.out / sm.vout as uint4
 template <bool KV = false>
-struct MgSmem {
+struct alignas(16) MgSmem {
     uint32_t in[MG_TILE];
-    uint32_t out[MG_TILE + MG_TILE / 32];
+    alignas(16) uint32_t out[MG_TILE + MG_TILE / 32];
     uint32_t vin[KV ? MG_TILE : 1];  // key/value: payloads of sm.in
-    uint32_t vout[KV ? MG_TILE + MG_TILE / 32 : 1];
+    alignas(16) uint32_t vout[KV ? MG_TILE + MG_TILE / 32 : 1];
 };
+static_assert(offsetof(MgSmem<false>, out) % 16 == 0 && offsetof(MgSmem<true>, vout) % 16 == 0, "uint4 LDS rows");
 
 // merge A[a0,a1) and B[b0,b1) (a1-a0 + b1-b0 <= MG_TILE) into out[0 ..)
 template <int BLOCK, int KPT>
@@ -1508,7 +1518,7 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
             // stored as 16-B nontemporal stores that each cover 1 KB -- no barrier.  Stored
             // straight from the registers, each lane's two 16-B stores at a 32-B lane stride
             // leave every wave-store half of each line: 0.486 ms per pass at 2^28 against
-            // 0.464 (r28, harness/exp/r4_mgx.sh).
+            // 0.464 (r28; the A/B launcher is in git history, commit 402e9ea).
             const uint32_t lane = tid & 63u, w = tid >> 6;
             uint32_t *wo = sm.out + w * 64u * KPT;
 #pragma unroll
@@ -1521,7 +1531,12 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
                     *reinterpret_cast<uint4 *>(wv + lane * KPT + 4 * j) =
                         make_uint4(pv[4 * j], pv[4 * j + 1], pv[4 * j + 2], pv[4 * j + 3]);
             }
-            u32x4 *o4 = reinterpret_cast<u32x4 *>(dst + cur.o0 + w * 64u * KPT);
+            // the read-back takes other lanes' words: order the wave's LDS writes before it
+            // (a wave's LDS operations complete in order on gfx950; this states it)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            u32x4 *o4 =reinterpret_cast<u32x4 *>(dst + cur.o0 + w * 64u * KPT);
 #pragma unroll
             for (int j = 0; j < KPT / 4; ++j) {
                 const uint4 v = *reinterpret_cast<const uint4 *>(wo + 4u * (lane + 64u * j));
@@ -1708,6 +1723,7 @@ static int cu_count() {
 
 hipError_t launch_onesweep_p(Bufs b, const Plan *plan, int pass, size_t n, uint32_t flip, const SegPlan *sp,
                              uint32_t *lookback, uint32_t *counter, uint32_t *err, hipStream_t s, const Bufs *vb) {
+    if (n > RADIX_MAX_N) return hipErrorInvalidValue;  // buffer descriptors: 4 n bytes < 2^32 (osp_rsrc)
     const size_t ntiles = (n + OSP_TILE - 1) / OSP_TILE + NSEG;
     const size_t want = (size_t)cu_count();  // one workgroup per CU (LDS-bound)
     const unsigned g = (unsigned)(ntiles < want ? ntiles : want);

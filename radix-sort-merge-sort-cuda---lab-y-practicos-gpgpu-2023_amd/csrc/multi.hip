@@ -20,6 +20,7 @@
 #include <dlfcn.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
@@ -389,9 +390,10 @@ struct Rccl {
     bool tried = false;
     void *h = nullptr;
     decltype(&ncclGetUniqueId) uid = nullptr;
-    decltype(&ncclCommInitRank) init_rank = nullptr;
-    decltype(&ncclCommInitAll) init_all = nullptr;
+    decltype(&ncclCommInitRankConfig) init_rank_cfg = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclCommAbort) abort = nullptr;
+    decltype(&ncclCommGetAsyncError) async_err = nullptr;
     decltype(&ncclAllGather) allgather = nullptr;
     decltype(&ncclSend) send = nullptr;
     decltype(&ncclRecv) recv = nullptr;
@@ -410,16 +412,18 @@ struct Rccl {
             return false;
         }
         uid = (decltype(uid))dlsym(h, "ncclGetUniqueId");
-        init_rank = (decltype(init_rank))dlsym(h, "ncclCommInitRank");
-        init_all = (decltype(init_all))dlsym(h, "ncclCommInitAll");
+        init_rank_cfg = (decltype(init_rank_cfg))dlsym(h, "ncclCommInitRankConfig");
         destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
+        abort = (decltype(abort))dlsym(h, "ncclCommAbort");
+        async_err = (decltype(async_err))dlsym(h, "ncclCommGetAsyncError");
         allgather = (decltype(allgather))dlsym(h, "ncclAllGather");
         send = (decltype(send))dlsym(h, "ncclSend");
         recv = (decltype(recv))dlsym(h, "ncclRecv");
         gstart = (decltype(gstart))dlsym(h, "ncclGroupStart");
         gend = (decltype(gend))dlsym(h, "ncclGroupEnd");
         errstr = (decltype(errstr))dlsym(h, "ncclGetErrorString");
-        if (!uid || !init_rank || !init_all || !destroy || !allgather || !send || !recv || !gstart || !gend) {
+        if (!uid || !init_rank_cfg || !destroy || !abort || !async_err || !allgather || !send || !recv || !gstart ||
+            !gend) {
             set_detail("RCCL: a symbol is missing from librccl.so");
             h = nullptr;
         }
@@ -441,11 +445,79 @@ Rccl g_rccl;
         if (_r != ncclSuccess) return g_rccl.fail(what, _r); \
     } while (0)
 
+// ---------------------------------------------------------------------------------
+// Bounded waits on RCCL.  Communicators are created nonblocking (ncclConfig_t
+// blocking = 0), so no RCCL call blocks the host: a call may return ncclInProgress and
+// the communicator is then polled (ncclCommGetAsyncError) until it settles, and a stream
+// carrying RCCL work is polled (hipStreamQuery) instead of synchronised.  Both polls
+// end at the communicator's deadline, or at once when an in-process peer reports a
+// failure: a rank whose peer never arrives -- its transport broke, or it left -- then
+// returns LABSORT_ERR_PEER instead of blocking forever, and its caller aborts the
+// communicator (ncclCommAbort), which stops its kernels and proxy thread.  (The
+// reference ends the process on any CUDA error, utils.h:18-26; here a failure ends every
+// rank's call and leaves the process usable.)
+// ---------------------------------------------------------------------------------
+constexpr double COMM_TIMEOUT_MS = 1000.0 * LABSORT_COMM_TIMEOUT_S;
+
+void poll_pause(double t0) {
+    if (now_ms() - t0 < 2.0) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(50));
+}
+int peer_gone(const char *what, const char *why) {
+    set_detail(std::string("RCCL ") + what + ": " + why + " (the communicator is aborted)");
+    t_last_hip = 0;
+    return LABSORT_ERR_PEER;
+}
+// the communicator's pending host-side work done (after a call that returned ncclInProgress)
+int rccl_settle(ncclComm_t c, double deadline, const char *what, const std::atomic<bool> *peer_failed = nullptr) {
+    const double t0 = now_ms();
+    for (;;) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t q = g_rccl.async_err(c, &st);
+        if (q != ncclSuccess) return g_rccl.fail(what, q);
+        if (st == ncclSuccess) return LABSORT_OK;
+        if (st != ncclInProgress) return g_rccl.fail(what, st);
+        if (peer_failed && peer_failed->load()) return peer_gone(what, "a peer rank failed");
+        if (now_ms() > deadline) return peer_gone(what, "timed out waiting for the peers");
+        poll_pause(t0);
+    }
+}
+// a nonblocking RCCL call: queued (ncclSuccess / ncclInProgress), then settled
+int rccl_call(ncclComm_t c, ncclResult_t r, double deadline, const char *what,
+              const std::atomic<bool> *peer_failed = nullptr) {
+    if (r != ncclSuccess && r != ncclInProgress) return g_rccl.fail(what, r);
+    return rccl_settle(c, deadline, what, peer_failed);
+}
+// stream s, which carries RCCL work of c, complete (the communicator's errors polled)
+int rccl_stream_wait(ncclComm_t c, hipStream_t s, double deadline, const char *what,
+                     const std::atomic<bool> *peer_failed = nullptr) {
+    const double t0 = now_ms();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return LABSORT_OK;
+        if (q != hipErrorNotReady) MHIP(q);
+        ncclResult_t st = ncclSuccess;
+        if (g_rccl.async_err(c, &st) != ncclSuccess || (st != ncclSuccess && st != ncclInProgress))
+            return g_rccl.fail(what, st);
+        if (peer_failed && peer_failed->load()) return peer_gone(what, "a peer rank failed");
+        if (now_ms() > deadline) return peer_gone(what, "timed out waiting for the peers");
+        poll_pause(t0);
+    }
+}
+ncclConfig_t nonblocking_config() {
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    return cfg;
+}
+
 // grouped pairwise send/recv with every peer at once: every xGMI link of the GPU
-// carries data together (the "pairwise RCCL send/recv merge" of the north_star)
+// carries data together (the "pairwise RCCL send/recv merge" of the north_star).  The
+// group is queued whole or not at all (ncclGroupEnd), then settled by the deadline.
 int rccl_exchange(ncclComm_t c, int p, int me, hipStream_t s, const uint32_t *const *send, const uint64_t *sc,
-                  uint32_t *const *recv, const uint64_t *rc) {
-    NCHK("ncclGroupStart", g_rccl.gstart());
+                  uint32_t *const *recv, const uint64_t *rc, double deadline,
+                  const std::atomic<bool> *peer_failed = nullptr) {
+    const ncclResult_t g = g_rccl.gstart();
+    if (g != ncclSuccess) return g_rccl.fail("ncclGroupStart", g);
     ncclResult_t bad = ncclSuccess;
     for (int j = 0; j < p && bad == ncclSuccess; ++j) {
         if (j == me) continue;
@@ -453,9 +525,8 @@ int rccl_exchange(ncclComm_t c, int p, int me, hipStream_t s, const uint32_t *co
         if (bad == ncclSuccess && rc[j]) bad = g_rccl.recv(recv[j], rc[j], ncclUint32, j, c, s);
     }
     const ncclResult_t e = g_rccl.gend();
-    if (bad != ncclSuccess) return g_rccl.fail("ncclSend/ncclRecv", bad);
-    if (e != ncclSuccess) return g_rccl.fail("ncclGroupEnd", e);
-    return LABSORT_OK;
+    if (bad != ncclSuccess && bad != ncclInProgress) return g_rccl.fail("ncclSend/ncclRecv", bad);
+    return rccl_call(c, e, deadline, "ncclGroupEnd (exchange)", peer_failed);
 }
 
 // ---------------------------------------------------------------------------------
@@ -467,12 +538,13 @@ struct ThreadShared {
     std::condition_variable cv;
     int arrived = 0;
     unsigned gen = 0;
-    bool failed = false;
+    std::atomic<bool> failed{false};
     std::vector<std::vector<uint8_t>> slot;
     std::vector<uint32_t *const *> rptr;  // each rank's receive addresses (during an exchange)
     std::vector<hipEvent_t> sent;          // each rank's "my sends are queued" event
     std::vector<int> dev;
     std::vector<ncclComm_t> comms;         // RCCL transport: one communicator per rank
+    double deadline = 0.0;                 // RCCL transport: the call's deadline (now_ms clock)
     explicit ThreadShared(int n) : p(n), slot(n), rptr(n, nullptr), sent(n, nullptr), dev(n, -1) {}
 
     // all ranks arrive; LABSORT_ERR_PEER if one of them failed without arriving (a rank
@@ -516,7 +588,7 @@ struct ThreadComm {
     }
     int exchange(const uint32_t *const *send, const uint64_t *sc, uint32_t *const *recv, const uint64_t *rc) {
         int st;
-        if (rccl) return rccl_exchange(sh.comms[me], sh.p, me, s, send, sc, recv, rc);
+        if (rccl) return rccl_exchange(sh.comms[me], sh.p, me, s, send, sc, recv, rc, sh.deadline, &sh.failed);
         // peer copies straight into each receiver's slot, on the sender's stream; the
         // receivers' streams then wait for every sender's event
         sh.rptr[me] = recv;
@@ -531,32 +603,69 @@ struct ThreadComm {
             if (i != me && rc[i]) MHIP(hipStreamWaitEvent(s, sh.sent[i], 0));
         return sh.barrier();  // the receive addresses are no longer read
     }
+    void abandon() { sh.abort(); }  // this rank leaves the exchange: its peers stop waiting now
 };
 
 // ---------------------------------------------------------------------------------
-// communicator 2: one process per rank over RCCL (ncclCommInitRank)
+// communicator 2: one process per rank over RCCL (ncclCommInitRankConfig, nonblocking)
 // communicator 3: host-staged callbacks (tests: torch.distributed gloo)
 // ---------------------------------------------------------------------------------
+struct RcclState {
+    ncclComm_t nc = nullptr;
+    bool broken = false;                   // aborted after a transport failure: every later call fails
+    double timeout_ms = COMM_TIMEOUT_MS;   // bound of every wait on the peers
+    Buf stage;                             // allgather staging, sized at init for the schedule's records
+    // abort after a transport failure (the peers' own waits then end at their deadlines)
+    void abort() {
+        if (nc) (void)g_rccl.abort(nc);
+        nc = nullptr;
+        broken = true;
+    }
+};
+// largest allgather of dist::sort_rank at p ranks, per rank: the sample record
+inline size_t stage_bytes(int p) { return (16 + 4 * dist::samples_per_rank(p)) * (size_t)(p + 1); }
+
 struct RcclComm {
-    ncclComm_t c;
+    RcclState &o;
     int p, me;
     hipStream_t s;
-    Buf &stage;
     int size() const { return p; }
     int rank() const { return me; }
+    int failed(int st) {
+        o.abort();
+        return st;
+    }
     int allgather(const void *in, void *out, size_t bytes) {
-        int st;
-        if ((st = grow(stage, bytes * (p + 1)))) return st;
-        uint8_t *d = as<uint8_t>(stage);
-        MHIP(hipMemcpyAsync(d + bytes * p, in, bytes, hipMemcpyHostToDevice, s));
-        NCHK("ncclAllGather", g_rccl.allgather(d + bytes * p, d, bytes, ncclUint8, c, s));
-        MHIP(hipMemcpyAsync(out, d, bytes * p, hipMemcpyDeviceToHost, s));
-        MHIP(hipStreamSynchronize(s));
-        return LABSORT_OK;
+        const double deadline = now_ms() + o.timeout_ms;
+        if (bytes * (p + 1) > o.stage.bytes) {  // (cannot happen: pre-sized for the schedule's records)
+            set_detail("RCCL allgather: record larger than the communicator's staging");
+            return failed(LABSORT_ERR_ARG);
+        }
+        uint8_t *d = as<uint8_t>(o.stage);
+        hipError_t h = hipMemcpyAsync(d + bytes * p, in, bytes, hipMemcpyHostToDevice, s);
+        if (h != hipSuccess) {
+            t_last_hip = (int)h;
+            set_detail(std::string("allgather staging: ") + hipGetErrorString(h));
+            return failed(LABSORT_ERR_HIP);
+        }
+        int st = rccl_call(o.nc, g_rccl.allgather(d + bytes * p, d, bytes, ncclUint8, o.nc, s), deadline,
+                           "ncclAllGather");
+        if (!st) {
+            h = hipMemcpyAsync(out, d, bytes * p, hipMemcpyDeviceToHost, s);
+            if (h != hipSuccess) {
+                t_last_hip = (int)h;
+                set_detail(std::string("allgather staging: ") + hipGetErrorString(h));
+                st = LABSORT_ERR_HIP;
+            }
+        }
+        if (!st) st = rccl_stream_wait(o.nc, s, deadline, "ncclAllGather");
+        return st ? failed(st) : LABSORT_OK;
     }
     int exchange(const uint32_t *const *send, const uint64_t *sc, uint32_t *const *recv, const uint64_t *rc) {
-        return rccl_exchange(c, p, me, s, send, sc, recv, rc);
+        const int st = rccl_exchange(o.nc, p, me, s, send, sc, recv, rc, now_ms() + o.timeout_ms);
+        return st ? failed(st) : LABSORT_OK;
     }
+    void abandon() { o.abort(); }  // a transport that breaks is gone for every later sort too
 };
 
 struct HostCbComm {
@@ -566,10 +675,11 @@ struct HostCbComm {
     std::vector<uint32_t> &hs, &hr;  // host staging of the key pieces
     int size() const { return p; }
     int rank() const { return me; }
+    // a failed callback: the caller's transport failed or a peer left it
     int allgather(const void *in, void *out, size_t bytes) {
         if (cb.allgather(cb.ctx, in, out, bytes)) {
             set_detail("labsort_host_coll.allgather failed");
-            return LABSORT_ERR_ARG;
+            return LABSORT_ERR_PEER;
         }
         return LABSORT_OK;
     }
@@ -592,7 +702,7 @@ struct HostCbComm {
         MHIP(hipStreamSynchronize(s));
         if (cb.alltoallv(cb.ctx, hs.data(), sb.data(), hr.data(), rb.data())) {
             set_detail("labsort_host_coll.alltoallv failed");
-            return LABSORT_ERR_ARG;
+            return LABSORT_ERR_PEER;
         }
         o = 0;
         for (int j = 0; j < p; ++j) {
@@ -602,28 +712,65 @@ struct HostCbComm {
         MHIP(hipStreamSynchronize(s));  // the staging buffer may be reused
         return LABSORT_OK;
     }
+    void abandon() {}  // the caller's collectives bound their own waits (gloo: the group's timeout)
 };
+
+// test hook of the schedule (labsort_test_fault; dist_plan.h dist::Fault)
+std::mutex g_fault_mu;
+dist::Fault g_fault;
+dist::Fault armed_fault() {
+    std::lock_guard<std::mutex> lk(g_fault_mu);
+    return g_fault;
+}
 
 // ---------------------------------------------------------------------------------
 // in-process ranks: labsort_sort_host_ranks
 // ---------------------------------------------------------------------------------
 std::mutex g_mu;                 // one in-process multi-GPU sort at a time
 std::vector<RankState> g_ranks;  // per rank slot, re-bound when its device changes
-std::vector<int> g_comm_devs;    // devices of the cached ncclCommInitAll communicators
+std::vector<int> g_comm_devs;    // devices of the cached in-process communicators
 std::vector<ncclComm_t> g_comms;
 double g_phase_ms[LABSORT_MULTI_PHASES];
 std::vector<dist::Result> g_res;  // each rank's collective times in the last call
 size_t g_sent_bytes = 0;
 std::vector<size_t> g_range_counts;  // keys of each rank's range in the last call
+double g_timeout_ms = COMM_TIMEOUT_MS;  // labsort_comm_set_timeout(NULL, s): in-process ranks, new communicators
 
-int rccl_comms(const std::vector<int> &devs) {
+// abort the cached in-process communicators (after a transport failure): recreated next call
+void drop_comms() {
+    for (ncclComm_t &c : g_comms)
+        if (c) (void)g_rccl.abort(c);
+    g_comms.clear();
+    g_comm_devs.clear();
+}
+
+// one nonblocking communicator per device, created from this thread in one group
+// (ncclCommInitRankConfig x p between ncclGroupStart/End), each settled by the deadline
+int rccl_comms(const std::vector<int> &devs, double deadline) {
     if (!g_rccl.load()) return LABSORT_ERR_HIP;
     if (g_comm_devs == devs) return LABSORT_OK;
     for (ncclComm_t c : g_comms)  // the device set changed: release the old communicators
         if (c) (void)g_rccl.destroy(c);
     g_comms.assign(devs.size(), nullptr);
     g_comm_devs.clear();
-    NCHK("ncclCommInitAll", g_rccl.init_all(g_comms.data(), (int)devs.size(), devs.data()));
+    ncclUniqueId u;
+    NCHK("ncclGetUniqueId", g_rccl.uid(&u));
+    ncclConfig_t cfg = nonblocking_config();
+    NCHK("ncclGroupStart", g_rccl.gstart());
+    ncclResult_t bad = ncclSuccess;
+    for (size_t r = 0; r < devs.size() && (bad == ncclSuccess || bad == ncclInProgress); ++r) {
+        MHIP(hipSetDevice(devs[r]));
+        bad = g_rccl.init_rank_cfg(&g_comms[r], (int)devs.size(), u, (int)r, &cfg);
+    }
+    const ncclResult_t e = g_rccl.gend();
+    int st = (bad != ncclSuccess && bad != ncclInProgress) ? g_rccl.fail("ncclCommInitRankConfig", bad)
+             : (e != ncclSuccess && e != ncclInProgress)   ? g_rccl.fail("ncclGroupEnd (init)", e)
+                                                           : LABSORT_OK;
+    for (size_t r = 0; r < devs.size() && !st; ++r) st = rccl_settle(g_comms[r], deadline, "ncclCommInitRankConfig");
+    if (st) {
+        drop_comms();
+        return st;
+    }
     g_comm_devs = devs;
     return LABSORT_OK;
 }
@@ -655,8 +802,10 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
         if (int st = bind_rank(g_ranks[r], devs[r])) return st;
     ThreadShared sh(p);
     sh.dev = devs;
-    if (transport == LABSORT_XFER_RCCL) {
-        if (int st = rccl_comms(devs)) return st;
+    const bool rccl = transport == LABSORT_XFER_RCCL;
+    sh.deadline = now_ms() + g_timeout_ms;
+    if (rccl) {
+        if (int st = rccl_comms(devs, sh.deadline)) return st;
         sh.comms = g_comms;
     } else {
         for (int a = 0; a < p; ++a)
@@ -685,6 +834,7 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
     std::vector<dist::Result> res(p);
     std::vector<std::vector<double>> ph(p, std::vector<double>(LABSORT_MULTI_PHASES, 0.0));
     const double t0 = now_ms();
+    const dist::Fault fault = armed_fault();
     std::vector<std::thread> th;
     th.reserve(p);
     for (int r = 0; r < p; ++r)
@@ -693,8 +843,19 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
             RankState &R = g_ranks[r];
             int e = hipSetDevice(R.dev) == hipSuccess ? LABSORT_OK : LABSORT_ERR_HIP;
             HipRankOps ops{R, R.own, key_type, true};
-            ThreadComm comm{sh, r, R.own, transport == LABSORT_XFER_RCCL};
-            if (!e) e = dist::sort_rank(ops, comm, h + off[r], off[r + 1] - off[r], flip, h, res[r]);
+            ThreadComm comm{sh, r, R.own, rccl};
+            if (!e) e = dist::sort_rank(ops, comm, h + off[r], off[r + 1] - off[r], flip, h, res[r], fault);
+            if (rccl) {
+                // the rank's RCCL work (its exchange) done, bounded by the deadline and by the
+                // peers' failures; a failed rank aborts its communicator before draining its
+                // streams, so none of its kernels waits for a peer that is gone
+                if (!e) e = rccl_stream_wait(sh.comms[r], R.own, sh.deadline, "exchange", &sh.failed);
+                if (e) {
+                    sh.abort();
+                    (void)g_rccl.abort(sh.comms[r]);
+                    sh.comms[r] = nullptr;
+                }
+            }
             const int f = ops.finish();  // drain the streams even after a failure
             if (!e) e = f;
             if (e) sh.abort();
@@ -704,6 +865,15 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
         });
     for (auto &t : th) t.join();
     const double t1 = now_ms();
+    if (rccl) {
+        bool any = false;
+        for (int r = 0; r < p; ++r) any = any || st[r];
+        if (any) {  // the aborted communicators (and the survivors of the failed call) go
+            for (int r = 0; r < p; ++r)
+                if (!sh.comms[r]) g_comms[r] = nullptr;
+            drop_comms();
+        }
+    }
     for (int r = 0; r < p; ++r) {
         (void)hipSetDevice(devs[r]);
         (void)hipEventDestroy(sent_ev[r]);
@@ -740,10 +910,9 @@ int sort_ranks(uint32_t *h, size_t n, int key_type, int p, const int *devices, i
 struct labsort_comm {
     int kind = 0;  // 1 RCCL, 2 host callbacks
     int p = 0, me = 0, dev = -1;
-    ncclComm_t nc = nullptr;
+    labsort::RcclState rc;  // RCCL: the nonblocking communicator, its deadline and staging
     labsort_host_coll cb{};
     labsort::RankState R;
-    labsort::Buf stage;
     std::vector<uint32_t> hs, hr;
     double phase[LABSORT_MULTI_PHASES] = {};
     labsort::dist::Result res;  // collective times of the last sort
@@ -861,18 +1030,51 @@ int labsort_comm_init_rccl(labsort_comm_t *comm, const void *id, int nranks, int
     c->kind = 1;
     c->p = nranks;
     c->me = rank;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        c->rc.timeout_ms = g_timeout_ms;
+    }
     if (hipGetDevice(&c->dev) != hipSuccess) {
         delete c;
         return LABSORT_ERR_HIP;
     }
+    // the allgather staging is sized here for the schedule's largest record, so nothing
+    // can fail between a rank's status word and its collective
+    if (int st = grow(c->rc.stage, stage_bytes(nranks))) {
+        delete c;
+        return st;
+    }
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
-    const ncclResult_t r = g_rccl.init_rank(&c->nc, nranks, u, rank);
-    if (r != ncclSuccess) {
+    ncclConfig_t cfg = nonblocking_config();
+    const ncclResult_t r = g_rccl.init_rank_cfg(&c->rc.nc, nranks, u, rank, &cfg);  // (sets rc.nc first)
+    const int st = rccl_call(c->rc.nc, r, now_ms() + c->rc.timeout_ms, "ncclCommInitRankConfig");
+    if (st) {  // (a peer that never joins: the deadline, then the half-made communicator aborted)
+        c->rc.abort();
+        (void)hipFree(c->rc.stage.p);
         delete c;
-        return g_rccl.fail("ncclCommInitRank", r);
+        return st;
     }
     *comm = c;
+    return LABSORT_OK;
+}
+
+int labsort_comm_set_timeout(labsort_comm_t c, double seconds) {
+    if (!(seconds > 0.0)) return LABSORT_ERR_ARG;
+    if (c) c->rc.timeout_ms = 1000.0 * seconds;
+    else {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_timeout_ms = 1000.0 * seconds;
+    }
+    return LABSORT_OK;
+}
+
+int labsort_test_fault(const char *phase, int rank) {
+    const int ph = dist::fault_phase(phase);
+    if (phase && !ph) return LABSORT_ERR_ARG;
+    std::lock_guard<std::mutex> lk(g_fault_mu);
+    g_fault.phase = ph;
+    g_fault.rank = ph ? rank : -1;
     return LABSORT_OK;
 }
 
@@ -896,14 +1098,14 @@ int labsort_comm_init_host(labsort_comm_t *comm, int nranks, int rank, const lab
 int labsort_comm_destroy(labsort_comm_t c) {
     if (!c) return LABSORT_OK;
     int st = LABSORT_OK;
-    if (c->nc) {
-        const ncclResult_t r = g_rccl.destroy(c->nc);
+    if (c->rc.nc) {
+        const ncclResult_t r = g_rccl.destroy(c->rc.nc);
         if (r != ncclSuccess) st = g_rccl.fail("ncclCommDestroy", r);
     }
     if (c->R.dev >= 0) {
         (void)hipSetDevice(c->R.dev);
         for (Buf *b : {&c->R.x, &c->R.y, &c->R.ws, &c->R.mws, &c->R.recv, &c->R.out, &c->R.small, &c->R.part,
-                       &c->R.errs, &c->stage})
+                       &c->R.errs, &c->rc.stage})
             if (b->p) (void)hipFree(b->p);
         for (hipStream_t s : {c->R.own, c->R.copy, c->R.plan})
             if (s) (void)hipStreamDestroy(s);
@@ -924,20 +1126,30 @@ int labsort_dist_sort(labsort_comm_t c, const void *d_keys, size_t m, int key_ty
     t_last_hip = 0;
     int cur = 0;
     if (hipGetDevice(&cur) != hipSuccess || cur != c->dev) return LABSORT_ERR_ARG;  // the comm's device
+    if (c->kind == 1 && c->rc.broken) {  // aborted after a transport failure in an earlier call
+        set_detail("RCCL communicator aborted by an earlier transport failure: create a new one");
+        return LABSORT_ERR_PEER;
+    }
     if (int st = bind_rank(c->R, c->dev)) return st;
     hipStream_t s = static_cast<hipStream_t>(stream);  // NULL: the null stream, as everywhere in the C-ABI
     HipRankOps ops{c->R, s, key_type, false};
     dist::Result res;
     const double t0 = now_ms();
+    const dist::Fault fault = armed_fault();
+    const uint32_t flip = key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u;
     int st;
     if (c->kind == 1) {
-        RcclComm comm{c->nc, c->p, c->me, s, c->stage};
-        st = dist::sort_rank(ops, comm, static_cast<const uint32_t *>(d_keys), m,
-                             key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u, nullptr, res);
+        RcclComm comm{c->rc, c->p, c->me, s};
+        st = dist::sort_rank(ops, comm, static_cast<const uint32_t *>(d_keys), m, flip, nullptr, res, fault);
+        // the exchange (queued on s) done, bounded: a peer that left ends this rank's wait at
+        // the deadline, and the aborted communicator stops its kernels before the drain below
+        if (!st && !c->rc.broken) {
+            st = rccl_stream_wait(c->rc.nc, s, now_ms() + c->rc.timeout_ms, "exchange");
+            if (st) c->rc.abort();
+        }
     } else {
         HostCbComm comm{c->cb, c->p, c->me, s, c->hs, c->hr};
-        st = dist::sort_rank(ops, comm, static_cast<const uint32_t *>(d_keys), m,
-                             key_type == LABSORT_KEY_I32 ? 0x80000000u : 0u, nullptr, res);
+        st = dist::sort_rank(ops, comm, static_cast<const uint32_t *>(d_keys), m, flip, nullptr, res, fault);
     }
     const int f = ops.finish();
     if (!st) st = f;

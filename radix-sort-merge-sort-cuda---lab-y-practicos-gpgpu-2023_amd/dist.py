@@ -296,5 +296,5 @@ def dist_sort_splitters(local: torch.Tensor, comm, key: str = "u32", stream=None
     sample, pairwise send/recv with every peer at once, merge of the received runs in
     rank order).  Returns (this rank's contiguous range of the sorted array, its global
     offset); copy=False: the range as a view of the communicator's buffer (kept alive by
-    the view, overwritten by the communicator's next sort)."""
+    the view, invalid after the communicator's next sort: see DistComm.sort_tensor)."""
     return comm.sort_tensor(local, local.numel(), key=key, stream=stream, copy=copy)

@@ -33,8 +33,22 @@ def free_port():
     return p
 
 
+def skewed_shard(O, rank, seed):
+    """rank 0: 200000 keys below 2^31; rank r > 0: 1000 keys above every key of the ranks
+    before it.  The samples are not weighted by shard size, so range 0 is all of shard 0:
+    past the pre-sized receive buffer (dist_plan.h recv_estimate), and the schedule takes
+    its growth round."""
+    if rank == 0:
+        return O.gen(200_000, seed, "u31")
+    return (O.gen(1000, seed, "u32", first=rank * 1000) & np.uint32(0x00FFFFFF)) | np.uint32(0x80000000 + (rank << 24))
+
+
 def _run_cfg(O, D, rank, world, cfg):
     m, dist_name, seed, key = cfg["m"], cfg["dist"], cfg["seed"], cfg["key"]
+    if cfg.get("skew"):
+        out, goff = O.dist_sort(skewed_shard(O, rank, seed), key, world, rank, D.GlooColl(),
+                                cap=200_000 + 1000 * world)
+        return out.view(np.int32).copy(), goff
     if cfg.get("exchange") == "splitters":
         sizes = cfg.get("sizes") or [m] * world
         first = sum(sizes[:rank])
@@ -143,12 +157,16 @@ CFGS = [
     dict(m=20000, dist="reversed", seed=8, key="u32", exchange="splitters", max_share=1.02),
     # ragged and empty shards (the last entries are cut to the world size)
     dict(m=3000, dist="u32", seed=9, key="u32", exchange="splitters", sizes=[0, 3000, 1, 7000, 0, 5, 2999, 0]),
+    # skewed shards: one range outgrows the pre-sized receive buffer (the growth round)
+    dict(m=0, dist="u32", seed=10, key="u32", exchange="splitters", skew=True),
 ]
 
 
 def _expected(oracle, world, cfg):
     """the whole array = the shards as the workers generate them, in rank order, sorted"""
-    if cfg.get("exchange") == "splitters":
+    if cfg.get("skew"):
+        full = np.concatenate([skewed_shard(oracle, r, cfg["seed"]) for r in range(world)])
+    elif cfg.get("exchange") == "splitters":
         sizes = cfg.get("sizes") or [cfg["m"]] * world
         full = np.concatenate([oracle.gen(sizes[r], cfg["seed"], cfg["dist"], first=sum(sizes[:r]))
                                for r in range(world)])
@@ -179,17 +197,19 @@ def test_dist_sort_gloo(oracle, world):
 def test_dist_sort_gloo_world8(oracle):
     """BASELINE config 5's rank count (8) on CPU: bitonic network and the product's
     splitter schedule."""
-    _check_world(oracle, 8, [0, 6, 11, 12, 13, 15])
+    _check_world(oracle, 8, [0, 6, 11, 12, 13, 15, 16])
 
 
 # ---- a failing rank ends every rank (labsort_dist_sort's failure agreement) ----------
-FAIL_CASES = [("local_sort", 1), ("bounds", 0), ("recv", -1)]  # -1: the last rank
+# (phase, failing rank; -1: the last rank).  "grow" runs on skewed shards, where every
+# rank takes the receive buffer's growth round.
+FAIL_CASES = [("local_sort", 1), ("bounds", 0), ("recv", -1), ("grow", 1)]
 
 
 def _fail_worker(rank, world, port, q):
-    """one rank: each failure case in turn (LABSORT_TEST_FAIL=<phase>:<rank>), then a
-    normal sort on the same gloo group -- which only works if every rank left the failed
-    sorts after the same collective"""
+    """one rank: each failure case in turn (oracle.test_fault(phase, rank): the test hook
+    of dist_plan.h), then a normal sort on the same gloo group -- which only works if
+    every rank left the failed sorts after the same collective"""
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -200,16 +220,18 @@ def _fail_worker(rank, world, port, q):
         import oracle as O
         D = importlib.import_module(PKG_NAME + ".dist")
         shard = O.gen(3000, 0x5EED0011, "u32", first=rank * 3000)
+        skew = skewed_shard(O, rank, 0x5EED0013)
         for ci, (phase, fr) in enumerate(FAIL_CASES):
-            os.environ["LABSORT_TEST_FAIL"] = f"{phase}:{fr % world}"
+            O.test_fault(phase, fr % world)
+            x = skew if phase == "grow" else shard
             t0 = time.monotonic()
             try:
-                O.dist_sort(shard, "u32", world, rank, D.GlooColl(), cap=3000 * world + 1)
+                O.dist_sort(x, "u32", world, rank, D.GlooColl(), cap=200_000 + 3000 * world)
                 status = 0
             except RuntimeError as e:
                 status = int(str(e).rsplit(" ", 1)[1])
             q.put((ci, rank, status, time.monotonic() - t0))
-        os.environ.pop("LABSORT_TEST_FAIL")
+        O.test_fault(None)
         out, goff = O.dist_sort(shard, "u32", world, rank, D.GlooColl(), cap=3000 * world + 1)
         q.put((len(FAIL_CASES), rank, 0, (out, goff)))
     finally:
@@ -218,10 +240,11 @@ def _fail_worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_dist_sort_failure_ends_every_rank(oracle, world):
-    """A rank whose local sort, bound queries or receive buffer fails reports its status in
-    the next collective: it returns its own error (LABSORT_ERR_DEVICE, 3) and every other
-    rank LABSORT_ERR_PEER (4), within seconds, instead of waiting for it; the group then
-    sorts normally (the ranks left after the same collective)."""
+    """A rank whose local sort, bound queries, receive buffer or buffer growth fails
+    reports its status in the next collective: it returns its own error
+    (LABSORT_ERR_DEVICE, 3) and every other rank LABSORT_ERR_PEER (4), within seconds,
+    instead of waiting for it; the group then sorts normally (the ranks left after the
+    same collective)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
@@ -244,6 +267,63 @@ def test_dist_sort_failure_ends_every_rank(oracle, world):
     parts = [got[(len(FAIL_CASES), r)][1] for r in range(world)]
     assert [g for _, g in parts] == list(np.cumsum([0] + [o.size for o, _ in parts])[:-1])
     np.testing.assert_array_equal(np.concatenate([o for o, _ in parts]), full)
+
+
+def _exchange_fail_worker(rank, world, port, q):
+    """one rank of a sort whose rank 1 leaves at the exchange without taking part (its
+    transport broke): the peers' gloo all-to-all must end (the group's 10 s timeout, or
+    the failed rank's connections closing) instead of hanging.  The group is unusable
+    afterwards, so the process ends without another collective."""
+    import datetime
+    import time
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=10))
+    import oracle as O
+    D = importlib.import_module(PKG_NAME + ".dist")
+    O.test_fault("exchange", 1)
+    t0 = time.monotonic()
+    try:
+        O.dist_sort(O.gen(3000, 0x5EED0014, "u32", first=rank * 3000), "u32", world, rank, D.GlooColl(),
+                    cap=3000 * world + 1)
+        status = 0
+    except RuntimeError as e:
+        status = int(str(e).rsplit(" ", 1)[1])
+    q.put((rank, status, time.monotonic() - t0))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_sort_exchange_failure_ends_every_rank(world):
+    """one rank fails inside the exchange (no status round follows it):
+    that rank returns LABSORT_ERR_DEVICE and every other rank a non-zero status
+    (LABSORT_ERR_PEER: the host collective failed) within 30 s."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_exchange_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, st, secs = q.get(timeout=120)
+        got[r] = (st, secs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        st, secs = got[r]
+        assert st == (3 if r == 1 else 4), (r, st)
+        assert secs < 30, (r, secs)
+
+
+def test_test_fault_phase_names(oracle):
+    """the schedule's test hook knows its five phases; unknown names disarm"""
+    for ph in ("local_sort", "bounds", "recv", "grow", "exchange", None, "nonsense"):
+        oracle.test_fault(ph, 0)
+    oracle.test_fault(None)
 
 
 def test_schedule_shape():

@@ -156,7 +156,19 @@ def test_dist_sort_rccl_one_rank(ls, oracle, torch_gpu):
 
 
 # ---- a failing rank ends every rank (the status words of dist_plan.h's collectives) ----
-FAIL_CASES = [("local_sort", 1), ("bounds", 0), ("recv", -1)]
+FAIL_CASES = [("local_sort", 1), ("bounds", 0), ("recv", -1), ("grow", 1)]
+
+
+def _skewed(ls, torch, rank, m):
+    """rank 0: m keys below 2^31; rank r > 0: 1000 keys above every key of the ranks
+    before it -- range 0 outgrows the pre-sized receive buffer (the growth round)"""
+    if rank == 0:
+        t = torch.empty(m, dtype=torch.int32, device="cuda")
+        ls.fill(t, m, 0x5EED0015, "u31")
+        return t
+    t = torch.empty(1000, dtype=torch.int32, device="cuda")
+    ls.fill(t, 1000, 0x5EED0015, "u32", first=rank * 1000)
+    return (t & 0x00FFFFFF) | ((0x80000000 + (rank << 24)) - (1 << 32))  # (the int32 of that word)
 
 
 def _fail_worker(rank, world, port, q):
@@ -175,16 +187,21 @@ def _fail_worker(rank, world, port, q):
         m = 200_000
         t = torch.empty(m, dtype=torch.int32, device="cuda")
         ls.fill(t, m, 0x5EED0012, "u32", first=rank * m)
+        skew = _skewed(ls, torch, rank, m)
         for ci, (phase, fr) in enumerate(FAIL_CASES):
-            os.environ["LABSORT_TEST_FAIL"] = f"{phase}:{fr % world}"
+            ls.test_fault(phase, fr % world)
+            x = skew if phase == "grow" else t
             t0 = time.monotonic()
             try:
-                comm.sort(t, m)
+                comm.sort(x, x.numel())
                 st = 0
             except ls.LabsortError as e:
                 st = e.status
             q.put((ci, rank, st, time.monotonic() - t0))
-        os.environ.pop("LABSORT_TEST_FAIL")
+        ls.test_fault(None)
+        out, goff = D.dist_sort_splitters(skew, comm)  # the growth round, then the sorted ranges
+        torch.cuda.synchronize()
+        q.put((len(FAIL_CASES) + 1, rank, 0, (out.cpu().numpy().copy(), goff)))
         out, goff = D.dist_sort_splitters(t, comm)  # the communicator still works
         torch.cuda.synchronize()
         q.put((len(FAIL_CASES), rank, 0, (out.cpu().numpy().copy(), goff)))
@@ -195,10 +212,10 @@ def _fail_worker(rank, world, port, q):
 
 @pytest.mark.parametrize("world", [2, 4])
 def test_dist_sort_failure_ends_every_rank(oracle, world):
-    """labsort_dist_sort with one rank's local sort, bound queries or receive buffer
-    failing (LABSORT_TEST_FAIL): that rank returns LABSORT_ERR_DEVICE, every other rank
-    LABSORT_ERR_PEER, each within seconds, and the next sort on the same communicators
-    succeeds."""
+    """labsort_dist_sort with one rank's local sort, bound queries, receive buffer or
+    buffer growth failing (ls.test_fault): that rank returns LABSORT_ERR_DEVICE, every
+    other rank LABSORT_ERR_PEER, each within seconds, and the next sorts on the same
+    communicators succeed (one of them on skewed shards, through the growth round)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
@@ -206,7 +223,7 @@ def test_dist_sort_failure_ends_every_rank(oracle, world):
     for p in procs:
         p.start()
     got = {}
-    for _ in range(world * (len(FAIL_CASES) + 1)):
+    for _ in range(world * (len(FAIL_CASES) + 2)):
         ci, r, st, extra = q.get(timeout=300)
         got[(ci, r)] = (st, extra)
     for p in procs:
@@ -221,6 +238,105 @@ def test_dist_sort_failure_ends_every_rank(oracle, world):
     exp = oracle.sort_u32(oracle.gen(m * world, 0x5EED0012, "u32"))
     np.testing.assert_array_equal(np.concatenate([got[(len(FAIL_CASES), r)][1][0] for r in range(world)]).view(np.uint32),
                                   exp)
+    # skewed shards: range 0 = all of shard 0, through the growth round
+    skew = [oracle.gen(m, 0x5EED0015, "u31")] + [
+        (oracle.gen(1000, 0x5EED0015, "u32", first=r * 1000) & np.uint32(0x00FFFFFF)) | np.uint32(0x80000000 + (r << 24))
+        for r in range(1, world)]
+    parts = [got[(len(FAIL_CASES) + 1, r)][1] for r in range(world)]
+    assert parts[0][0].size == m and [g for _, g in parts] == list(np.cumsum([0] + [o.size for o, _ in parts])[:-1])
+    np.testing.assert_array_equal(np.concatenate([o for o, _ in parts]).view(np.uint32),
+                                  oracle.sort_u32(np.concatenate(skew)))
+
+
+def _exchange_fail_worker(rank, world, port, q):
+    """rank 1 leaves at the exchange without taking part (ls.test_fault("exchange", 1)):
+    the peers' host-staged all-to-all must end (gloo timeout 10 s, or the failed rank's
+    connections closing); the group is unusable afterwards, so the process just ends"""
+    import datetime
+    import time
+    sys.path.insert(0, REPO)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=10))
+    ls = importlib.import_module(PKG_NAME)
+    D = importlib.import_module(PKG_NAME + ".dist")
+    comm = D.make_comm(ls, backend="gloo")
+    m = 100_000
+    t = torch.empty(m, dtype=torch.int32, device="cuda")
+    ls.fill(t, m, 0x5EED0016, "u32", first=rank * m)
+    ls.test_fault("exchange", 1)
+    t0 = time.monotonic()
+    try:
+        comm.sort(t, m)
+        st = 0
+    except ls.LabsortError as e:
+        st = e.status
+    torch.cuda.synchronize()
+    q.put((rank, st, time.monotonic() - t0))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_sort_exchange_failure_ends_every_rank(world):
+    """VERDICT r4 item 3 on the HIP instantiation (host-staged communicator over gloo): one
+    rank fails inside the exchange; it returns LABSORT_ERR_DEVICE, every other rank
+    LABSORT_ERR_PEER, all within 30 s."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_exchange_fail_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(world):
+        r, st, secs = q.get(timeout=180)
+        got[r] = (st, secs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in range(world):
+        st, secs = got[r]
+        assert st == (3 if r == 1 else 4), (r, st)
+        assert secs < 30, (r, secs)
+
+
+def _rccl_init_alone(q):
+    """rank 0 of a 2-rank RCCL communicator whose rank 1 never joins: the nonblocking
+    ncclCommInitRankConfig must end at the communicator deadline (3 s here) with
+    LABSORT_ERR_PEER, not block forever"""
+    import time
+    sys.path.insert(0, REPO)
+    import torch
+    torch.cuda.set_device(0)
+    ls = importlib.import_module(PKG_NAME)
+    ls.set_comm_timeout(3.0)
+    uid = ls.DistComm.unique_id()
+    t0 = time.monotonic()
+    try:
+        ls.DistComm.rccl(2, 0, uid)
+        st = 0
+    except ls.LabsortError as e:
+        st = e.status
+    q.put((st, time.monotonic() - t0))
+    q.close()
+    q.join_thread()
+    os._exit(0)
+
+
+def test_rccl_init_peer_never_joins():
+    """RCCL communicator creation is bounded: a peer that never joins ends the wait at the
+    deadline (LABSORT_ERR_PEER) and the half-made communicator is aborted."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_init_alone, args=(q,))
+    p.start()
+    st, secs = q.get(timeout=120)
+    p.join(timeout=60)
+    assert st == 4, st
+    assert 2.5 < secs < 30, secs
 
 
 def test_bench_dist_gloo_config5():

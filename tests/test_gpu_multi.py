@@ -61,19 +61,48 @@ def test_sort_host_ranks_rccl_one_rank(ls, oracle, torch_gpu):
     np.testing.assert_array_equal(b, oracle.sort_u32(a))
 
 
-@pytest.mark.parametrize("phase", ["local_sort", "bounds", "recv"])
-def test_sort_host_ranks_rank_failure(ls, oracle, torch_gpu, monkeypatch, phase):
-    """one in-process rank failing (LABSORT_TEST_FAIL) ends the call with that rank's own
-    error (LABSORT_ERR_DEVICE), not a hang; the next call works"""
-    monkeypatch.setenv("LABSORT_TEST_FAIL", f"{phase}:2")
+@pytest.mark.parametrize("phase", ["local_sort", "bounds", "recv", "exchange"])
+def test_sort_host_ranks_rank_failure(ls, oracle, torch_gpu, phase):
+    """one in-process rank failing (ls.test_fault, the schedule's test hook; "exchange": it
+    leaves without taking part) ends the call with that rank's own error
+    (LABSORT_ERR_DEVICE), not a hang; the next call works"""
+    import time
     a = oracle.gen(300_000, 0x5EED7500, "u32")
-    with pytest.raises(ls.LabsortError) as e:
-        ls.sort_host_ranks(a.copy(), [0] * 4, transport="peer")
-    assert e.value.status == ls.ERR_DEVICE
-    monkeypatch.delenv("LABSORT_TEST_FAIL")
+    ls.test_fault(phase, 2)
+    try:
+        t0 = time.monotonic()
+        with pytest.raises(ls.LabsortError) as e:
+            ls.sort_host_ranks(a.copy(), [0] * 4, transport="peer")
+        assert e.value.status == ls.ERR_DEVICE
+        assert time.monotonic() - t0 < 30
+    finally:
+        ls.test_fault(None)
     b = a.copy()
     ls.sort_host_ranks(b, [0] * 4, transport="peer")
     np.testing.assert_array_equal(b, oracle.sort_u32(a))
+
+
+def test_sort_host_ranks_rccl_one_rank_fault(ls, oracle, torch_gpu):
+    """the RCCL transport (nonblocking communicators, bounded waits): a rank failing at its
+    local sort returns its error, the communicators are recreated and the next call works"""
+    a = oracle.gen((1 << 18) + 3, 0x5EED7401, "u32")
+    ls.test_fault("local_sort", 0)
+    try:
+        with pytest.raises(ls.LabsortError) as e:
+            ls.sort_host_ranks(a.copy(), [0], transport="rccl")
+        assert e.value.status == ls.ERR_DEVICE
+    finally:
+        ls.test_fault(None)
+    b = a.copy()
+    ls.sort_host_ranks(b, [0], transport="rccl")
+    np.testing.assert_array_equal(b, oracle.sort_u32(a))
+
+
+def test_test_fault_rejects_unknown_phase(ls):
+    with pytest.raises(ls.LabsortError) as e:
+        ls.test_fault("nonsense", 0)
+    assert e.value.status == ls.ERR_ARG
+    ls.test_fault(None)
 
 
 def test_sort_host_multi_arg_checks(ls, torch_gpu):
