@@ -658,6 +658,7 @@ def main():
         torch.cuda.synchronize()
         m1 = time.perf_counter()
         mp_ms, mp_cnt = ls.timing_read("merge")
+        m4_ms, m4_cnt = ls.timing_read("merge4")
         ts_ms, ts_cnt = ls.timing_read("tile_sort")
         ls.timing_enable(False)
         ls.workspace_status(mws, n, "merge", stream=stream)
@@ -666,20 +667,32 @@ def main():
             print("bench.py: MERGE OUTPUT CHECK FAILED", file=sys.stderr)
             sys.exit(3)
         mavg = mp_ms / mp_cnt if mp_cnt else None
+        m4avg = m4_ms / m4_cnt if m4_cnt else None
         tavg = ts_ms / ts_cnt if ts_cnt else None
         mtraffic, msrc = pmc_traffic("merge", n)
+        m4traffic, m4src = pmc_traffic("merge4", n)
         ttraffic, _ = pmc_traffic("tile_sort", n)
+
+        def pass_roofline(kernel, avg, traffic, src):
+            return {"bound": "hbm", "kernel": kernel, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "avg_launch_ms": round(avg, 5) if avg else None,
+                    "achieved": round(8.0 * n / (avg * 1e-3) / 1e9, 1) if avg else None,
+                    "frac": round(8.0 * n / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if avg else None,
+                    "algorithmic_bytes_per_launch": 8.0 * n, "traffic": traffic, "traffic_source": src}
+        # dominant merge kernel: the four-way pass (two merge levels per read and write of the
+        # keys; its launch = k_m4_rank + k_m4_merge), the pairwise pass when no four-way ran
+        four = bool(m4_cnt)
         merge_leg = {
-            "workload": f"LDS tile sort + merge-path passes of the same 2^{args.log2n} device-resident keys "
-                        "(BASELINE config 4)",
+            "workload": f"LDS tile sort + merge passes (four-way, one pairwise for an odd level count) of the same "
+                        f"2^{args.log2n} device-resident keys (BASELINE config 4)",
             "value": round(n * args.steps / (m1 - m0) / 1e6, 2), "unit": "Mkeys/s",
-            "ms_per_step": round((m1 - m0) / args.steps * 1e3, 4), "passes_per_sort": mp_cnt // max(args.steps, 1),
+            "ms_per_step": round((m1 - m0) / args.steps * 1e3, 4),
+            "passes_per_sort": (mp_cnt + m4_cnt) // max(args.steps, 1),
+            "four_way_passes_per_sort": m4_cnt // max(args.steps, 1),
             "verified": "sorted permutation (descents, digit histograms, sums)",
-            "roofline": {"bound": "hbm", "kernel": "k_merge_pass_p", "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "avg_launch_ms": round(mavg, 5) if mavg else None,
-                         "achieved": round(8.0 * n / (mavg * 1e-3) / 1e9, 1) if mavg else None,
-                         "frac": round(8.0 * n / (mavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if mavg else None,
-                         "algorithmic_bytes_per_launch": 8.0 * n, "traffic": mtraffic, "traffic_source": msrc},
+            "roofline": (pass_roofline("k_m4_rank + k_m4_merge", m4avg, m4traffic, m4src) if four
+                         else pass_roofline("k_merge_pass_p", mavg, mtraffic, msrc)),
+            "pairwise_pass": pass_roofline("k_merge_pass_p", mavg, mtraffic, msrc) if four and mavg else None,
             "tile_sort": {"kernel": "k_tile_sort", "avg_launch_ms": round(tavg, 5) if tavg else None,
                           "achieved": round(8.0 * n / (tavg * 1e-3) / 1e9, 1) if tavg else None,
                           "frac": round(8.0 * n / (tavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if tavg else None,
@@ -755,7 +768,7 @@ def main():
                      "value": round(n * args.steps / (p1 - p0) / 1e6, 2), "unit": "Mpairs/s",
                      "ms_per_step": round((p1 - p0) / args.steps * 1e3, 4),
                      "verified": "sorted, payload = input index of its key, equal keys in input order",
-                     "roofline": {"bound": "hbm", "kernel": "k_onesweep_p<2, false, true>", "peak": HBM_PEAK_GBS,
+                     "roofline": {"bound": "hbm", "kernel": "k_onesweep_p<true> (key/value)", "peak": HBM_PEAK_GBS,
                                   "unit": "GB/s", "avg_launch_ms": round(pavg, 5) if pavg else None,
                                   "achieved": round(16.0 * n / (pavg * 1e-3) / 1e9, 1) if pavg else None,
                                   "frac": round(16.0 * n / (pavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pavg else None,
@@ -831,7 +844,7 @@ def main():
         "roofline": roofline, "cpu_baseline": cpu,
     }
     for leg in (merge_leg and merge_leg["roofline"], merge_leg and merge_leg["tile_sort"],
-                pairs_leg and pairs_leg["roofline"]):  # each leg's dominant kernel against the same copy
+                merge_leg and merge_leg.get("pairwise_pass"), pairs_leg and pairs_leg["roofline"]):  # each leg's dominant kernel against the same copy
         if leg and leg.get("achieved"):
             leg["copy_frac"] = round(leg["achieved"] / copy_gbs, 4)
     if merge_leg:

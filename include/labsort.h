@@ -81,7 +81,8 @@ extern "C" {
 #define LABSORT_K_GSWEEP 5       /* gathered radix pass (LABSORT_ALGO_RADIX, 2^16 <= n < 2^25) */
 #define LABSORT_K_GCOPY 6        /* its final gathered copy */
 #define LABSORT_K_COPY 7         /* the streaming copy (labsort_copy: the bench's copy ceiling) */
-#define LABSORT_K_COUNT 8
+#define LABSORT_K_MERGE4 8       /* four-way merge pass of the merge sort (k_m4_rank + k_m4_merge) */
+#define LABSORT_K_COUNT 9
 
 /* ---- library info ---- */
 const char *labsort_version(void);

@@ -31,7 +31,7 @@ ALGO = {"radix": 0, "merge": 1, "radix1": 2, "auto": 3}
 KEY = {"u32": 0, "i32": 1}
 DIST = {"u32": 0, "u31": 1, "mod100": 2, "mod1000": 3, "sorted": 4, "reversed": 5, "const": 6, "lowbits": 7}
 KCLASS = {"histogram": 0, "onesweep": 1, "tile_sort": 2, "merge": 3, "partition": 4, "gsweep": 5, "gcopy": 6,
-          "copy": 7}
+          "copy": 7, "merge4": 8}
 
 # exported symbols of include/labsort.h + lab.h (checked by tests/test_abi.py)
 C_SYMBOLS = [

@@ -10,6 +10,7 @@
 // as CUDA_CHK/gpuAssert do (utils.h:30-38).  The extern "C" API returns codes.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -129,8 +130,20 @@ RadixLayout radix_layout(size_t n, int bits, size_t tile) {
     return L;
 }
 
+// Merge sort levels after the tile sort: runs of TS_TILE keys doubled until one run.
+// LABSORT_MERGE4 (build knob, default 1): two levels per four-way pass (merge4.hip), the odd
+// level first as a pairwise pass; 0: pairwise passes only.
+#ifndef LABSORT_MERGE4
+#define LABSORT_MERGE4 1
+#endif
+int merge_levels(size_t n) {
+    int m = 0;
+    for (size_t run = TS_TILE; run < n; run *= 2) ++m;
+    return m;
+}
+
 struct MergeLayout {
-    size_t off_tmp, off_part, total;
+    size_t off_tmp, off_part, off_bnd, total;
 };
 MergeLayout merge_layout(size_t n) {
     MergeLayout L{};
@@ -139,6 +152,11 @@ MergeLayout merge_layout(size_t n) {
     o = align_up(o + n * 4, 256);
     L.off_part = o;
     o = align_up(o + (labsort_merge_parts(n)) * 4, 256);
+    L.off_bnd = o;
+    size_t bw = 0;  // the four-way passes' boundary tables (one at a time)
+    if (LABSORT_MERGE4)
+        for (size_t r = (merge_levels(n) % 2 ? 2 : 1) * (size_t)TS_TILE; r < n; r *= 4) bw = std::max(bw, merge4_bnd_words(n, r));
+    o = align_up(o + bw * 4, 256);
     L.total = o;
     return L;
 }
@@ -228,32 +246,38 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
     return LABSORT_OK;
 }
 
-// Pairwise merge-path passes after the tile sort (runs of TS_TILE keys).  A K-way pass
-// (K = 4, 8: 5 passes instead of 13 at 2^28) was built and measured slower on MI355X
-// (9.7-14 ms vs 7.9 ms: LDS-operation bound) and removed.
-int merge_passes(size_t n) {
-    int m = 0;
-    for (size_t run = TS_TILE; run < n; run *= 2) ++m;
-    return m;
-}
-
+// Merge passes after the tile sort (runs of TS_TILE keys): four-way passes (two levels per
+// HBM read and write, merge4.hip) and, for an odd level count, one pairwise merge-path pass
+// first.  (An earlier K-way pass, LDS merges with binary searches per key, measured slower
+// than pairwise passes: 9.7-14 vs 7.9 ms)
 int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s) {
     const MergeLayout L = merge_layout(n);
     uint32_t *tmp = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
     uint32_t *part = reinterpret_cast<uint32_t *>(ws + L.off_part);
-    const int m = merge_passes(n);
-    uint32_t *cur = (m % 2 == 0) ? out : tmp;
+    uint32_t *bnd = reinterpret_cast<uint32_t *>(ws + L.off_bnd);
+    const int m = merge_levels(n);
+    const bool four = LABSORT_MERGE4 && (((uintptr_t)out | (uintptr_t)tmp) & 15u) == 0;
+    const int npass = four ? m / 2 + m % 2 : m;
+    uint32_t *cur = (npass % 2 == 0) ? out : tmp;
     {
         TimingScope ts(LABSORT_K_TILE_SORT, s);
         HIP_TRY(launch_tile_sort(in, cur, n, flip, s));
     }
     size_t run = TS_TILE;
-    for (int k = 0; k < m; ++k) {
+    for (int lv = 0; lv < m;) {
         uint32_t *nxt = (cur == out) ? tmp : out;
-        TimingScope ts(LABSORT_K_MERGE, s);
-        HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s));
+        if (four && (m - lv) % 2 == 0) {
+            TimingScope ts(LABSORT_K_MERGE4, s);
+            HIP_TRY(launch_merge4_pass(cur, nxt, n, run, flip, bnd, s));
+            run *= 4;
+            lv += 2;
+        } else {
+            TimingScope ts(LABSORT_K_MERGE, s);
+            HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s));
+            run *= 2;
+            lv += 1;
+        }
         cur = nxt;
-        run *= 2;
     }
     return LABSORT_OK;
 }

@@ -61,7 +61,11 @@ struct SegPlan {
 // than 8192-key runs; measured 9.45 -> 8.60 ms for the 2^28 merge sort (r11).
 constexpr int TS_BLOCK = 1024;
 constexpr int TS_KPT = 32;
-constexpr int TS_TILE = TS_BLOCK * TS_KPT;  // sorted run length of the tile sort
+#ifndef LABSORT_TS_KBLOCK
+#define LABSORT_TS_KBLOCK 1024  // keys-only tile sort threads (A/B build knob: 512 = 16K-key tiles, 2 per CU)
+#endif
+constexpr int TS_KBLOCK = LABSORT_TS_KBLOCK;
+constexpr int TS_TILE = TS_KBLOCK * TS_KPT;  // sorted run length of the tile sort
 // key/value tile sort: keys and payloads both in LDS (2 x 64 KB)
 constexpr int TS_KPT_KV = 16;
 constexpr int TS_TILE_KV = TS_BLOCK * TS_KPT_KV;
@@ -165,6 +169,11 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
                              const MgPairs *pairs = nullptr);
 hipError_t launch_tile_sort_kv(const uint32_t *in, uint32_t *out, const uint32_t *vin, uint32_t *vout, size_t n,
                                uint32_t flip, hipStream_t s);
+// four-way merge pass (merge4.hip): runs of r keys (a multiple of 128) -> runs of 4r;
+// bnd: merge4_bnd_words(n, r) words of workspace (16-B aligned); out 16-B aligned
+size_t merge4_bnd_words(size_t n, size_t r);
+hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_t r, uint32_t flip, uint32_t *bnd,
+                              hipStream_t s);
 hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size_t lb, uint32_t *out, size_t d0,
                            size_t d1, uint32_t flip, uint32_t *part, hipStream_t s);
 hipError_t launch_upper_bound(const uint32_t *keys, size_t n, uint32_t flip, const uint32_t *values, size_t nv,

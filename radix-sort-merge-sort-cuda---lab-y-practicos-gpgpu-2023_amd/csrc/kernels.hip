@@ -885,7 +885,16 @@ void k_onesweep_p(Bufs bufs, const Plan *__restrict__ plan, int pass, uint32_t n
             load_tile(cB, kB);
             if constexpr (KV) load_vals(cB, vB);
         }
-        if (haveB) {  // stable wave rank of B
+        // key/value: the lane-order check hoisted out of the key loop (r29, same box: 0.899 vs
+        // 0.909 ms per pass, r27's 0.899; for keys only it measured slower, 0.485 vs 0.466:
+        // profiles/r29_ab_rank_hoist.txt)
+        if (KV && haveB && atomic_rank) {  // stable wave rank of B
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t r = wave_atomic_rank(wh, ((kB[j] ^ flip) >> shift) & 255u, lane);
+                rB[j / 2] = (j & 1) ? rB[j / 2] | (r << 16) : r;
+            }
+        } else if (haveB) {  // stable wave rank of B
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t d = ((kB[j] ^ flip) >> shift) & 255u;
@@ -1790,7 +1799,7 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) 
 hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t nt = (n + TS_TILE - 1) / TS_TILE;
-    k_tile_sort<TS_BLOCK, TS_KPT><<<(unsigned)nt, TS_BLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
+    k_tile_sort<TS_KBLOCK, TS_KPT><<<(unsigned)nt, TS_KBLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
     return hipGetLastError();
 }
 
