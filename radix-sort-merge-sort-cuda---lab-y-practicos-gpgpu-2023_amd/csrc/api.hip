@@ -143,7 +143,7 @@ int merge_levels(size_t n) {
 }
 
 struct MergeLayout {
-    size_t off_tmp, off_part, off_bnd, total;
+    size_t off_tmp, off_part, off_bnd, off_samp[2], total;
 };
 MergeLayout merge_layout(size_t n) {
     MergeLayout L{};
@@ -157,6 +157,10 @@ MergeLayout merge_layout(size_t n) {
     if (LABSORT_MERGE4)
         for (size_t r = (merge_levels(n) % 2 ? 2 : 1) * (size_t)TS_TILE; r < n; r *= 4) bw = std::max(bw, merge4_bnd_words(n, r));
     o = align_up(o + bw * 4, 256);
+    for (int i = 0; i < 2; ++i) {  // the four-way passes' samples, written by the pass before (ping-pong)
+        L.off_samp[i] = o;
+        if (bw) o = align_up(o + merge4_samp_words(n) * 4, 256);
+    }
     L.total = o;
     return L;
 }
@@ -259,21 +263,28 @@ int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char 
     const bool four = LABSORT_MERGE4 && (((uintptr_t)out | (uintptr_t)tmp) & 15u) == 0;
     const int npass = four ? m / 2 + m % 2 : m;
     uint32_t *cur = (npass % 2 == 0) ? out : tmp;
+    // samples for a four-way pass are written by the pass before it (samp[0], samp[1] in turn)
+    uint32_t *samp[2] = {reinterpret_cast<uint32_t *>(ws + L.off_samp[0]), reinterpret_cast<uint32_t *>(ws + L.off_samp[1])};
+    int sb = 0;
+    auto next_is_four = [&](int lv) { return four && lv < m && (m - lv) % 2 == 0; };
     {
         TimingScope ts(LABSORT_K_TILE_SORT, s);
-        HIP_TRY(launch_tile_sort(in, cur, n, flip, s));
+        HIP_TRY(launch_tile_sort(in, cur, n, flip, s, next_is_four(0) ? samp[sb] : nullptr));
     }
     size_t run = TS_TILE;
     for (int lv = 0; lv < m;) {
         uint32_t *nxt = (cur == out) ? tmp : out;
-        if (four && (m - lv) % 2 == 0) {
+        if (next_is_four(lv)) {
             TimingScope ts(LABSORT_K_MERGE4, s);
-            HIP_TRY(launch_merge4_pass(cur, nxt, n, run, flip, bnd, s));
+            HIP_TRY(launch_merge4_pass(cur, nxt, n, run, flip, bnd, samp[sb], next_is_four(lv + 2) ? samp[sb ^ 1] : nullptr,
+                                       s));
+            sb ^= 1;
             run *= 4;
             lv += 2;
         } else {
             TimingScope ts(LABSORT_K_MERGE, s);
-            HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s));
+            HIP_TRY(launch_merge_pass(cur, nxt, n, run, flip, part, s, nullptr, nullptr, nullptr,
+                                      next_is_four(lv + 1) ? samp[sb] : nullptr));
             run *= 2;
             lv += 1;
         }

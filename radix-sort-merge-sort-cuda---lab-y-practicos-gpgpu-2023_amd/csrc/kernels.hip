@@ -1096,7 +1096,8 @@ struct TsSmem {
 // VGPRs, 3 spilled; profiles/r28_ab_tile_sort_precheck.txt).
 template <int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint32_t *out, const uint32_t *vin,
-                                                         uint32_t *vout, uint32_t n, uint32_t flip) {
+                                                         uint32_t *vout, uint32_t n, uint32_t flip,
+                                                         uint32_t *samp_out = nullptr) {
     using S = TsSmem<BLOCK, KPT, KV>;
     constexpr int R = S::R, W = S::W, TILE = S::TILE;
     __shared__ S sm;
@@ -1225,6 +1226,15 @@ __global__ __launch_bounds__(BLOCK, 4) void k_tile_sort(const uint32_t *in, uint
         }
         // (the next pass's reorder writes sm.keys two barriers later)
     }
+    // samp_out: every M4_S-th output key for a four-way merge pass next (merge4.hip)
+    static_assert((KPT * WAVE) % M4_S == 0 && M4_S % WAVE == 0, "samples at lane 0 of fixed slots");
+    if (samp_out && lane == 0) {
+#pragma unroll
+        for (int j = 0; j < KPT; ++j) {
+            const uint32_t idx = wbase + j * WAVE;
+            if (((uint32_t)j * WAVE) % M4_S == 0 && idx < n) samp_out[idx / M4_S] = k[j];
+        }
+    }
     if (full) {
 #pragma unroll
         for (int j = 0; j < KPT; ++j) out[wbase + j * WAVE] = k[j];
@@ -1288,9 +1298,14 @@ __device__ __forceinline__ uint32_t corank(const uint32_t *A, uint32_t la, const
 }
 
 // 16-B aligned: the full-tile path reads and writes sm.out / sm.vout as uint4
+#ifndef LABSORT_MG_PAD
+#define LABSORT_MG_PAD 1
+#endif
+constexpr bool MG_PAD = LABSORT_MG_PAD != 0;  // keys-only merge pass: +inf pads after both runs in LDS
+constexpr uint32_t MG_PADW = 8;
 template <bool KV = false>
 struct alignas(16) MgSmem {
-    uint32_t in[MG_TILE];
+    uint32_t in[MG_TILE + 2 * MG_PADW];
     alignas(16) uint32_t out[MG_TILE + MG_TILE / 32];
     uint32_t vin[KV ? MG_TILE : 1];  // key/value: payloads of sm.in
     alignas(16) uint32_t vout[KV ? MG_TILE + MG_TILE / 32 : 1];
@@ -1370,7 +1385,8 @@ template <int BLOCK, int KPT, bool KV = false>
 __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                         uint32_t n, uint32_t run, uint32_t flip, uint32_t ntiles,
                                                         uint32_t m, MgPairs pr, const uint32_t *__restrict__ vsrc = nullptr,
-                                                        uint32_t *__restrict__ vdst = nullptr) {
+                                                        uint32_t *__restrict__ vdst = nullptr,
+                                                        uint32_t *__restrict__ samp_out = nullptr) {
     constexpr uint32_t T = (uint32_t)(BLOCK * KPT);
     static_assert(T == (uint32_t)MG_TILE, "tile granularity");
     __shared__ MgSmem<KV> sm;
@@ -1445,8 +1461,20 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
     load(cur, nx, nv);
     for (uint32_t t = t0; t < t1; ++t) {
         __syncthreads();  // previous tile's merge no longer reads sm.in
+        if constexpr (!KV && MG_PAD) {
+            // keys only: A | MG_PADW words of +inf | B | MG_PADW words of +inf, so the network's
+            // windows need no bounds checks (the keys-only merge is VALU-bound: r29)
 #pragma unroll
-        for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
+            for (int j = 0; j < KPT; ++j) {
+                const uint32_t i = tid + (uint32_t)j * BLOCK;
+                sm.in[i + (i >= cur.la ? MG_PADW : 0u)] = nx[j];
+            }
+            if (tid < 2u * MG_PADW)
+                sm.in[(tid < MG_PADW ? cur.la : cur.tot + MG_PADW) + tid % MG_PADW] = ~flip;  // +inf in key order
+        } else {
+#pragma unroll
+            for (int j = 0; j < KPT; ++j) sm.in[tid + (uint32_t)j * BLOCK] = nx[j];
+        }
         if constexpr (KV) {
 #pragma unroll
             for (int j = 0; j < KPT; ++j) sm.vin[tid + (uint32_t)j * BLOCK] = nv[j];
@@ -1470,15 +1498,21 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
             // (A ascending, B reversed), instead of KPT dependent LDS reads with a branch
             // each: 0.458 -> 0.437 ms per pass at 2^28 (r28, profiles/r28_ab_merge_network.txt;
             // a copy in place of any merge: 0.424)
-            const uint32_t ai = corank(sa, la, sb, lb, d, flip), bi = d - ai;
+            const uint32_t pb = la + (MG_PAD ? MG_PADW : 0u);  // B's LDS offset
+            const uint32_t ai = corank(sa, la, sm.in + pb, lb, d, flip), bi = d - ai;
             uint32_t x[2 * KPT];
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t ia = ai + (uint32_t)j, ib = bi + (uint32_t)j;
-                const uint32_t va = sm.in[min(ia, T - 1u)] ^ flip;       // sa = sm.in
-                const uint32_t vb = sm.in[min(la + ib, T - 1u)] ^ flip;  // sb = sm.in + la
-                x[j] = ia < la ? va : 0xFFFFFFFFu;
-                x[2 * KPT - 1 - j] = ib < lb ? vb : 0xFFFFFFFFu;
+                if constexpr (MG_PAD) {  // the pads end both windows
+                    x[j] = sm.in[ia] ^ flip;
+                    x[2 * KPT - 1 - j] = sm.in[pb + ib] ^ flip;
+                } else {
+                    const uint32_t va = sm.in[min(ia, T - 1u)] ^ flip;       // sa = sm.in
+                    const uint32_t vb = sm.in[min(la + ib, T - 1u)] ^ flip;  // sb = sm.in + la
+                    x[j] = ia < la ? va : 0xFFFFFFFFu;
+                    x[2 * KPT - 1 - j] = ib < lb ? vb : 0xFFFFFFFFu;
+                }
             }
 #pragma unroll
             for (int s = KPT; s >= 1; s >>= 1) {
@@ -1545,11 +1579,18 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            u32x4 *o4 =reinterpret_cast<u32x4 *>(dst + cur.o0 + w * 64u * KPT);
+            u32x4 *o4 = reinterpret_cast<u32x4 *>(dst + cur.o0 + w * 64u * KPT);
 #pragma unroll
             for (int j = 0; j < KPT / 4; ++j) {
                 const uint4 v = *reinterpret_cast<const uint4 *>(wo + 4u * (lane + 64u * j));
                 __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, o4 + lane + 64u * j);
+            }
+            // samp_out: every M4_S-th output key for a four-way pass next (merge4.hip): the
+            // wave's 64 KPT outputs hold 64 KPT / M4_S of them, one store by as many lanes
+            if constexpr (!KV) {
+                static_assert((64 * KPT) % M4_S == 0 && (uint32_t)MG_TILE % M4_S == 0, "samples per wave");
+                if (samp_out && lane < 64u * KPT / M4_S)
+                    samp_out[(cur.o0 + w * 64u * KPT) / M4_S + lane] = wo[M4_S * lane];
             }
             if constexpr (KV) {
                 const uint32_t *wv = sm.vout + w * 64u * KPT;
@@ -1576,7 +1617,10 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
 #pragma unroll
         for (int j = 0; j < KPT; ++j) {
             const uint32_t i = tid + (uint32_t)j * BLOCK;
-            if (i < tot) o[i] = sm.out[i + (i >> 5)];
+            if (i < tot) {
+                o[i] = sm.out[i + (i >> 5)];
+                if (!KV && samp_out && ((cur.o0 + i) & (M4_S - 1u)) == 0u) samp_out[(cur.o0 + i) / M4_S] = sm.out[i + (i >> 5)];
+            }
         }
         if constexpr (KV) {
             uint32_t *__restrict__ ov = vdst + cur.o0;
@@ -1796,10 +1840,12 @@ hipError_t launch_final_copy(Bufs b, const Plan *plan, size_t n, hipStream_t s) 
     return hipGetLastError();
 }
 
-hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s) {
+hipError_t launch_tile_sort(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, hipStream_t s,
+                            uint32_t *samp_out) {
     if (n == 0) return hipSuccess;
     const size_t nt = (n + TS_TILE - 1) / TS_TILE;
-    k_tile_sort<TS_KBLOCK, TS_KPT><<<(unsigned)nt, TS_KBLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip);
+    k_tile_sort<TS_KBLOCK, TS_KPT><<<(unsigned)nt, TS_KBLOCK, 0, s>>>(in, out, nullptr, nullptr, (uint32_t)n, flip,
+                                                                     samp_out);
     return hipGetLastError();
 }
 
@@ -1811,7 +1857,8 @@ hipError_t launch_wave_tile_sort(uint32_t *keys, size_t n, uint32_t flip, hipStr
 }
 
 hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t run, uint32_t flip,
-                             uint32_t *part, hipStream_t s, const uint32_t *vin, uint32_t *vout, const MgPairs *pairs) {
+                             uint32_t *part, hipStream_t s, const uint32_t *vin, uint32_t *vout, const MgPairs *pairs,
+                             uint32_t *samp_out) {
     MgPairs pr{};
     if (pairs) pr = *pairs;
     if (n == 0) return hipSuccess;
@@ -1825,7 +1872,8 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
         k_merge_pass_p<MG_BLOCK, MG_KPT, true>
             <<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr, vin, vout);
     else
-        k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr);
+        k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr,
+                                                                nullptr, nullptr, samp_out);
     return hipGetLastError();
 }
 

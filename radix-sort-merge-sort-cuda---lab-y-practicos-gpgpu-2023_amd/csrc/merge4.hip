@@ -30,13 +30,14 @@
 
 namespace labsort {
 
-constexpr uint32_t M4_S = 128;   // sample stride (keys)
+// M4_S (common.h): sample stride (keys)
 constexpr uint32_t M4_M = 28;    // samples per block (merged order)
 constexpr int M4_BLOCK = 512;    // threads per merge workgroup
 constexpr int M4_KPT = 8;        // outputs per thread and merge level
 constexpr uint32_t M4_CAP = (uint32_t)(M4_BLOCK * M4_KPT);  // keys per block at most
 static_assert((M4_M + 3) * M4_S <= M4_CAP - 2 * M4_KPT, "a block (and its level-1 padding) fits one pass of the threads");
 constexpr int M4_BLOCKS_PER_CU = 4;
+constexpr uint32_t M4_MAX_PER = 256;  // most consecutive blocks per merge workgroup (their cuts held in LDS)
 
 struct M4Geo {
     uint32_t n, r;        // keys, input run length (a multiple of M4_S)
@@ -94,29 +95,37 @@ __global__ __launch_bounds__(256) void k_m4_rank(const uint32_t *__restrict__ sr
     if ((uint64_t)q * M4_S >= len[k]) return;  // past a short last run
     const uint32_t *gb = src + (size_t)g * 4u * G.r;
     const uint32_t x = samp[sid];
-    // samples of the other runs that precede (x, k) in (key, run) order
-    uint32_t cnt[4];
-    uint32_t m = q;
+    // samples of the other runs that precede (x, k) in (key, run) order: upper bound in the
+    // runs before k, lower bound in the runs after it.  The three searches run interleaved,
+    // branch-free, one probe of each per step, so the thread waits on one chain of
+    // log2(r / M4_S) dependent loads instead of three in a row.
+    const uint32_t xf = x ^ flip;
+    uint32_t cnt[4], ns[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         cnt[j] = 0u;
-        if ((uint32_t)j == k || !len[j]) continue;
-        const uint32_t *rj = samp + (size_t)g * G.spg + (size_t)j * spr;
-        const uint32_t ns = (len[j] + M4_S - 1) / M4_S;
-        const bool le = (uint32_t)j < k;
-        uint32_t lo = 0, hi = ns;
-        const uint32_t xf = x ^ flip;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            const uint32_t v = rj[mid] ^ flip;
-            if (v < xf || (le && v == xf)) lo = mid + 1u;
-            else hi = mid;
-        }
-        cnt[j] = lo;
-        m += lo;
+        ns[j] = (uint32_t)j == k ? 0u : (len[j] + M4_S - 1) / M4_S;
     }
+    for (uint32_t step = 1u << (31 - __builtin_clz(spr)); step; step >>= 1) {
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t p = cnt[j] + step;
+            v[j] = p <= ns[j] ? samp[(size_t)g * G.spg + (size_t)j * spr + p - 1u] ^ flip : 0xFFFFFFFFu;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t p = cnt[j] + step;
+            const bool le = (uint32_t)j < k;
+            if (p <= ns[j] && (v[j] < xf || (le && v[j] == xf))) cnt[j] = p;
+        }
+    }
+    const uint32_t m = q + cnt[0] + cnt[1] + cnt[2] + cnt[3];
     if (m == 0u || m % M4_M != 0u) return;
-    // a boundary: its cut in every run (in run j, between the last preceding sample and the next)
+    // a boundary: its cut in every run -- in run j between the last preceding sample and the
+    // next, so within one sample gap (one in M4_M threads gets here; an interleaved
+    // branch-free form of these three searches stopped at the gap's start on the device when
+    // every sample of the run preceded, r29)
     uint32_t cut[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -135,9 +144,10 @@ __global__ __launch_bounds__(256) void k_m4_rank(const uint32_t *__restrict__ sr
     bnd[(size_t)g * G.bpg + m / M4_M] = make_uint4(cut[0], cut[1], cut[2], cut[3]);
 }
 
-// merge-path co-rank in LDS: A elements among the first d of merge(A, B)
-__device__ __forceinline__ uint32_t m4_corank(const uint32_t *A, uint32_t la, const uint32_t *B, uint32_t lb, uint32_t d,
-                                              uint32_t flip) {
+// merge-path co-rank in LDS: A elements among the first d of merge(A, B) (FLIP: int32 order)
+template <bool FLIP>
+__device__ __forceinline__ uint32_t m4_corank(const uint32_t *A, uint32_t la, const uint32_t *B, uint32_t lb, uint32_t d) {
+    constexpr uint32_t flip = FLIP ? 0x80000000u : 0u;
     uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;
     while (lo < hi) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -147,31 +157,42 @@ __device__ __forceinline__ uint32_t m4_corank(const uint32_t *A, uint32_t la, co
     return lo;
 }
 
-// 8 consecutive LDS words base[i .. i + 8) by three 16-B reads of the aligned 12 words around
-// them (a lane's window starts anywhere; as ds_read_b32 x 8 the lanes' windows, ~4 words
-// apart, hit the same banks 4 ways -- as ds_read_b128 they are contiguous 16-B slots)
+// 8 consecutive LDS words base[i .. i + 8) by five 8-B reads of the 10 words from i rounded
+// down to even, and one select per word (the pass is VALU-bound: r29 counters; 16-B reads
+// needed three selects per word, 4-B reads hit the lanes' shared banks 4 ways)
 __device__ __forceinline__ void m4_read8(const uint32_t *base, uint32_t i, uint32_t (&w)[M4_KPT]) {
-    const uint32_t a = i & ~3u, ph = i & 3u;
-    const uint4 *p = reinterpret_cast<const uint4 *>(base + a);
-    const uint4 q0 = p[0], q1 = p[1], q2 = p[2];
-    const uint32_t b[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+    const uint32_t a = i & ~1u;
+    const bool odd = (i & 1u) != 0u;
+    const uint2 *p = reinterpret_cast<const uint2 *>(base + a);
+    uint32_t b[M4_KPT + 2];
 #pragma unroll
-    for (int j = 0; j < M4_KPT; ++j)
-        w[j] = ph == 0 ? b[j] : ph == 1 ? b[j + 1] : ph == 2 ? b[j + 2] : b[j + 3];
+    for (int q = 0; q < M4_KPT / 2 + 1; ++q) {
+        const uint2 v = p[q];
+        b[2 * q] = v.x;
+        b[2 * q + 1] = v.y;
+    }
+    // (a bit select: as `odd ? b[j + 1] : b[j]` the compiler indexed b[] dynamically through
+    // the scratch stack)
+    const uint32_t m = odd ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int j = 0; j < M4_KPT; ++j) w[j] = (b[j] & ~m) | (b[j + 1] & m);
 }
 
-// the 8 smallest of A[ai, ai + 8) and B[bi, bi + 8) (flipped domain, ascending; entries past
-// la / lb count as +inf), by a bitonic merge of A ascending with B descending.  A and B are
-// offsets into the LDS buffer `buf` (16-B aligned, readable 12 words past any window).
-__device__ __forceinline__ void m4_window_merge(const uint32_t *buf, uint32_t A, uint32_t la, uint32_t ai, uint32_t B,
-                                                uint32_t lb, uint32_t bi, uint32_t flip, uint32_t (&r)[M4_KPT]) {
+// the 8 smallest of A[ai, ai + 8) and B[bi, bi + 8), by a bitonic merge of A ascending with B
+// descending.  A and B are LDS word offsets into `buf` (8-B aligned); each run is followed by
+// 8 pad words of +inf, so the windows need no bounds (equal keys are identical words: a pad
+// equal to a key changes no output).
+template <bool FLIP>
+__device__ __forceinline__ void m4_window_merge(const uint32_t *buf, uint32_t A, uint32_t ai, uint32_t B, uint32_t bi,
+                                                uint32_t (&r)[M4_KPT]) {
+    constexpr uint32_t flip = FLIP ? 0x80000000u : 0u;
     uint32_t wa[M4_KPT], wb[M4_KPT], x[2 * M4_KPT];
     m4_read8(buf, A + ai, wa);
     m4_read8(buf, B + bi, wb);
 #pragma unroll
     for (int j = 0; j < M4_KPT; ++j) {
-        x[j] = ai + (uint32_t)j < la ? wa[j] ^ flip : 0xFFFFFFFFu;
-        x[2 * M4_KPT - 1 - j] = bi + (uint32_t)j < lb ? wb[j] ^ flip : 0xFFFFFFFFu;
+        x[j] = wa[j] ^ flip;
+        x[2 * M4_KPT - 1 - j] = wb[j] ^ flip;
     }
 #pragma unroll
     for (int s = M4_KPT; s >= 1; s >>= 1) {
@@ -188,9 +209,11 @@ __device__ __forceinline__ void m4_window_merge(const uint32_t *buf, uint32_t A,
     for (int j = 0; j < M4_KPT; ++j) r[j] = x[j] ^ flip;
 }
 
+constexpr uint32_t M4_PAD = M4_KPT;  // +inf words after every run in LDS
 struct alignas(16) M4Smem {
-    alignas(16) uint32_t in[M4_CAP + 16];   // the block's windows A | B | C | D; then the output staging
-    alignas(16) uint32_t mid[M4_CAP + 32];  // level 1: A+B at 0, C+D at 8 ceil(lab / 8)
+    alignas(16) uint32_t in[M4_CAP + 4 * M4_PAD + 16];  // A | pad | B | pad | C | pad | D | pad; then the output staging
+    alignas(16) uint32_t mid[M4_CAP + 4 * M4_PAD + 16]; // level 1: A+B | pad | C+D | pad
+    uint4 lo[M4_MAX_PER + 1];                           // each of the workgroup's blocks' start cuts (read once, at entry)
 };
 
 struct M4Blk {
@@ -200,7 +223,9 @@ struct M4Blk {
     uint32_t tot;
 };
 
-__device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *bnd, uint32_t id) {
+// block id's geometry; lo = the LDS table of the workgroup's start cuts, t = id's entry in it
+// (the next entry is the block's end when it is in the same group)
+__device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *lo, uint32_t id, uint32_t t) {
     M4Blk q;
     const uint32_t g = id / G.bpg, b = id % G.bpg;
     uint32_t rl[4];
@@ -210,8 +235,13 @@ __device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *bnd, uint
 #pragma unroll
     for (int j = 0; j < 4; ++j) ns += (rl[j] + M4_S - 1) / M4_S;
     const uint32_t nb = (ns + M4_M - 1) / M4_M;
-    const uint4 l4 = b ? bnd[id] : make_uint4(0u, 0u, 0u, 0u);
-    const uint4 h4 = b + 1u < nb ? bnd[id + 1u] : make_uint4(rl[0], rl[1], rl[2], rl[3]);
+    // (workgroup-uniform: readfirstlane keeps the geometry in SGPRs)
+    auto uni = [](uint4 v) {
+        return make_uint4(__builtin_amdgcn_readfirstlane(v.x), __builtin_amdgcn_readfirstlane(v.y),
+                          __builtin_amdgcn_readfirstlane(v.z), __builtin_amdgcn_readfirstlane(v.w));
+    };
+    const uint4 l4 = uni(lo[t]);
+    const uint4 h4 = b + 1u < nb ? uni(lo[t + 1u]) : make_uint4(rl[0], rl[1], rl[2], rl[3]);
     q.lo[0] = l4.x, q.lo[1] = l4.y, q.lo[2] = l4.z, q.lo[3] = l4.w;
     q.len[0] = h4.x - l4.x, q.len[1] = h4.y - l4.y, q.len[2] = h4.z - l4.z, q.len[3] = h4.w - l4.w;
     q.g = g;
@@ -227,22 +257,28 @@ __device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *bnd, uint
     return q;
 }
 
+// LABSORT_M4_DIAG (timing builds only, wrong output): 1 = level 1 skipped, 2 = level 2
+// skipped (level 1's result stored), 3 = co-rank searches replaced by d / 2
+#ifndef LABSORT_M4_DIAG
+#define LABSORT_M4_DIAG 0
+#endif
 // workgroup: blocks [b0, b1) of the flat list in turn
+template <bool FLIP>
 __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
-                                                          M4Geo G, uint32_t flip, const uint4 *__restrict__ bnd,
-                                                          uint32_t per) {
+                                                          M4Geo G, const uint4 *__restrict__ bnd, uint32_t per,
+                                                          uint32_t *__restrict__ samp_out) {
+    constexpr uint32_t PADV = FLIP ? 0x7FFFFFFFu : 0xFFFFFFFFu;  // +inf in key order
     __shared__ M4Smem sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t b0 = blockIdx.x * per;
     if (b0 >= G.nblocks) return;
     const uint32_t b1 = b0 + per < G.nblocks ? b0 + per : G.nblocks;
-    // keys of block q into registers: LDS slot tid + j BLOCK of the windows A | B | C | D.
+    // keys of block q into registers: element tid + j BLOCK of the windows A | B | C | D.
     // (Each window's source address is a running select over the four, not an index into
     // q.lo[]: a dynamic index put the four bases on the scratch stack, one scratch load per key.)
     auto load = [&](const M4Blk &q, uint32_t (&v)[M4_KPT]) {
         const uint32_t o1 = q.len[0], o2 = o1 + q.len[1], o3 = o2 + q.len[2];
         const uint32_t *gb = src + (size_t)q.g * 4u * G.r;
-        // window k starts at gb + k r + lo[k], LDS slot o_k: address of slot i = base_k + i
         const uint32_t *b0 = gb + q.lo[0], *b1 = gb + G.r + q.lo[1] - o1, *b2 = gb + 2u * G.r + q.lo[2] - o2,
                        *b3 = gb + 3u * G.r + q.lo[3] - o3;
 #pragma unroll
@@ -255,47 +291,66 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
             v[j] = i < q.tot ? ld_stream<NT_MERGE>(a + i) : 0u;
         }
     };
+    // the start cuts of blocks b0 .. b1 (a group's first block starts at 0) into LDS: one
+    // global round trip here instead of one before every block's key loads
+    for (uint32_t t = tid; t <= b1 - b0; t += M4_BLOCK) {
+        const uint32_t id = b0 + t;
+        sm.lo[t] = (id < G.nblocks && id % G.bpg) ? bnd[id] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
     uint32_t nx[M4_KPT];
-    M4Blk cur = m4_block(G, bnd, b0);
+    M4Blk cur = m4_block(G, sm.lo, b0, 0u);
     load(cur, nx);
     for (uint32_t id = b0; id < b1; ++id) {
+        const uint32_t la = cur.len[0], lb = cur.len[1], lc = cur.len[2], ld = cur.len[3];
+        const uint32_t oB = la + M4_PAD, oC = oB + lb + M4_PAD, oD = oC + lc + M4_PAD;  // LDS offsets (A at 0)
         __syncthreads();  // the previous block's output staging (sm.in) has been stored
 #pragma unroll
-        for (int j = 0; j < M4_KPT; ++j) sm.in[tid + (uint32_t)j * M4_BLOCK] = nx[j];
+        for (int j = 0; j < M4_KPT; ++j) {
+            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
+            const uint32_t k = (i >= la) + (i >= la + lb) + (i >= la + lb + lc);  // window of element i
+            if (i < cur.tot) sm.in[i + k * M4_PAD] = nx[j];
+        }
+        if (tid < 4u * M4_PAD) {  // the pads
+            const uint32_t k = tid / M4_PAD, e = tid % M4_PAD;
+            const uint32_t end = k == 0 ? la : k == 1 ? oB + lb : k == 2 ? oC + lc : oD + ld;
+            sm.in[end + e] = PADV;
+        }
         M4Blk nxt = cur;
         if (id + 1u < b1) {
-            nxt = m4_block(G, bnd, id + 1u);
+            nxt = m4_block(G, sm.lo, id + 1u, id + 1u - b0);
             load(nxt, nx);
         }
         __syncthreads();  // sm.in holds the block
-        const uint32_t la = cur.len[0], lb = cur.len[1], lc = cur.len[2], ld = cur.len[3];
-        const uint32_t lab = la + lb, lcd = lc + ld, nab = (lab + M4_KPT - 1) / M4_KPT;
-        const uint32_t cdo = nab * M4_KPT;  // C+D's offset in sm.mid
+        const uint32_t lab = la + lb, lcd = lc + ld, nab = (lab + M4_KPT - 1) / M4_KPT, ncd = (lcd + M4_KPT - 1) / M4_KPT;
+        const uint32_t cdo = nab * M4_KPT + M4_PAD;  // C+D's offset in sm.mid
         // level 1: A+B (threads < nab) and C+D
         {
             const bool ab = tid < nab;
             const uint32_t d = (ab ? tid : tid - nab) * M4_KPT;
-            const uint32_t oA = ab ? 0u : lab, oB = oA + (ab ? la : lc);
-            const uint32_t l1 = ab ? la : lc, l2 = ab ? lb : ld, lt = l1 + l2;
-            if (d < lt) {
-                const uint32_t ai = m4_corank(sm.in + oA, l1, sm.in + oB, l2, d, flip);
+            const uint32_t oX = ab ? 0u : oC, oY = ab ? oB : oD;
+            const uint32_t l1 = ab ? la : lc, l2 = ab ? lb : ld;
+            if (LABSORT_M4_DIAG != 1 && d < l1 + l2) {
+                const uint32_t ai = LABSORT_M4_DIAG == 3 ? min(d / 2, l1) : m4_corank<FLIP>(sm.in + oX, l1, sm.in + oY, l2, d);
                 uint32_t r[M4_KPT];
-                m4_window_merge(sm.in, oA, l1, ai, oB, l2, d - ai, flip, r);
+                m4_window_merge<FLIP>(sm.in, oX, ai, oY, d - ai, r);
                 uint32_t *o = sm.mid + (ab ? 0u : cdo) + d;
 #pragma unroll
                 for (int j = 0; j < M4_KPT; j += 4)
                     *reinterpret_cast<uint4 *>(o + j) = make_uint4(r[j], r[j + 1], r[j + 2], r[j + 3]);
             }
+            if (tid < 2u * M4_PAD)  // pads after A+B's and C+D's last 8-word rows
+                sm.mid[(tid < M4_PAD ? nab * M4_KPT : cdo + ncd * M4_KPT) + tid % M4_PAD] = PADV;
         }
         __syncthreads();  // sm.mid holds A+B and C+D; sm.in is free
         // level 2: (A+B)+(C+D) into the staging buffer (16-B writes at the thread's diagonal)
         const uint32_t tot = cur.tot, ph = cur.out & 3u;
         {
             const uint32_t d = tid * M4_KPT;
-            if (d < tot) {
-                const uint32_t ai = m4_corank(sm.mid, lab, sm.mid + cdo, lcd, d, flip);
+            if (LABSORT_M4_DIAG != 2 && d < tot) {
+                const uint32_t ai = LABSORT_M4_DIAG == 3 ? min(d / 2, lab) : m4_corank<FLIP>(sm.mid, lab, sm.mid + cdo, lcd, d);
                 uint32_t r[M4_KPT];
-                m4_window_merge(sm.mid, 0u, lab, ai, cdo, lcd, d - ai, flip, r);
+                m4_window_merge<FLIP>(sm.mid, 0u, ai, cdo, d - ai, r);
 #pragma unroll
                 for (int j = 0; j < M4_KPT; j += 4)
                     *reinterpret_cast<uint4 *>(sm.in + d + j) = make_uint4(r[j], r[j + 1], r[j + 2], r[j + 3]);
@@ -306,15 +361,22 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
         // partial chunks at both ends by words
         const uint32_t nch = (ph + tot + 3u) / 4u;
         uint32_t *ob = dst + (cur.out - ph);
+        // (samp_out: the next four-way pass's samples, every M4_S-th output word)
+        const uint32_t obase = cur.out - ph;
         for (uint32_t c = tid; c < nch; c += M4_BLOCK) {
             const uint32_t w0 = 4u * c;
             if (w0 >= ph && w0 + 4u <= ph + tot) {
                 const uint32_t *sw = sm.in + (w0 - ph);
                 __builtin_nontemporal_store(u32x4{sw[0], sw[1], sw[2], sw[3]}, reinterpret_cast<u32x4 *>(ob + w0));
+                if (samp_out && ((obase + w0) & (M4_S - 1u)) == 0u) samp_out[(obase + w0) / M4_S] = sw[0];
             } else {
 #pragma unroll
                 for (uint32_t e = 0; e < 4u; ++e)
-                    if (w0 + e >= ph && w0 + e < ph + tot) ob[w0 + e] = sm.in[w0 + e - ph];
+                    if (w0 + e >= ph && w0 + e < ph + tot) {
+                        ob[w0 + e] = sm.in[w0 + e - ph];
+                        if (samp_out && ((obase + w0 + e) & (M4_S - 1u)) == 0u)
+                            samp_out[(obase + w0 + e) / M4_S] = sm.in[w0 + e - ph];
+                    }
             }
         }
         cur = nxt;
@@ -349,13 +411,17 @@ size_t merge4_bnd_words(size_t n, size_t r) {
 }
 
 hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_t r, uint32_t flip, uint32_t *bnd,
-                              hipStream_t s) {
+                              const uint32_t *samp_in, uint32_t *samp_out, hipStream_t s) {
     if (n == 0) return hipSuccess;
     if (r % M4_S || n > 0xFFFFFFFFull - 4 * r) return hipErrorInvalidValue;
     const M4Geo G = m4_geo(n, r);
     const size_t nsamp = (size_t)G.ngroups * G.spg;
-    uint32_t *samp = bnd + (size_t)G.ngroups * G.bpg * 4;
-    k_m4_sample<<<(unsigned)((nsamp + 255) / 256), 256, 0, s>>>(in, G, samp);
+    const uint32_t *samp = samp_in;
+    if (!samp) {  // no pass before wrote them: gathered here
+        uint32_t *own = bnd + (size_t)G.ngroups * G.bpg * 4;
+        k_m4_sample<<<(unsigned)((nsamp + 255) / 256), 256, 0, s>>>(in, G, own);
+        samp = own;
+    }
     k_m4_rank<<<(unsigned)((nsamp + 255) / 256), 256, 0, s>>>(in, G, flip, samp, reinterpret_cast<uint4 *>(bnd));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -363,9 +429,13 @@ hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint32_t want = (uint32_t)(M4_BLOCKS_PER_CU * (cus > 0 ? cus : 256));
-    const uint32_t per = (G.nblocks + want - 1) / want;
+    uint32_t per = (G.nblocks + want - 1) / want;
+    if (per > M4_MAX_PER) per = M4_MAX_PER;
     const uint32_t g = (G.nblocks + per - 1) / per;
-    k_m4_merge<<<g, M4_BLOCK, 0, s>>>(in, out, G, flip, reinterpret_cast<const uint4 *>(bnd), per);
+    if (flip)
+        k_m4_merge<true><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out);
+    else
+        k_m4_merge<false><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out);
     return hipGetLastError();
 }
 
