@@ -1467,7 +1467,7 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
 #pragma unroll
             for (int j = 0; j < KPT; ++j) {
                 const uint32_t i = tid + (uint32_t)j * BLOCK;
-                sm.in[i + (i >= cur.la ? MG_PADW : 0u)] = nx[j];
+                if (i < cur.tot) sm.in[i + (i >= cur.la ? MG_PADW : 0u)] = nx[j];  // (not over B's pads)
             }
             if (tid < 2u * MG_PADW)
                 sm.in[(tid < MG_PADW ? cur.la : cur.tot + MG_PADW) + tid % MG_PADW] = ~flip;  // +inf in key order

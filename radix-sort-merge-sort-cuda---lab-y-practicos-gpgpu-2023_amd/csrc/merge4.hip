@@ -32,8 +32,8 @@ namespace labsort {
 
 // M4_S (common.h): sample stride (keys)
 constexpr uint32_t M4_M = 28;    // samples per block (merged order)
-constexpr int M4_BLOCK = 512;    // threads per merge workgroup
-constexpr int M4_KPT = 8;        // outputs per thread and merge level
+constexpr int M4_KPT = 8;                // outputs per thread and merge level (r29: 16, with 256
+constexpr int M4_BLOCK = 4096 / M4_KPT;  // threads and half the co-rank searches, measured equal)
 constexpr uint32_t M4_CAP = (uint32_t)(M4_BLOCK * M4_KPT);  // keys per block at most
 static_assert((M4_M + 3) * M4_S <= M4_CAP - 2 * M4_KPT, "a block (and its level-1 padding) fits one pass of the threads");
 constexpr int M4_BLOCKS_PER_CU = 4;
@@ -82,69 +82,153 @@ __global__ __launch_bounds__(256) void k_m4_sample(const uint32_t *__restrict__ 
     samp[sid] = pos < G.n ? ld_stream<NT_MERGE>(src + pos) : 0u;
 }
 
-// one thread per sample: merged-order index; boundaries (every M4_M-th) write their cuts
-__global__ __launch_bounds__(256) void k_m4_rank(const uint32_t *__restrict__ src, M4Geo G, uint32_t flip,
-                                                 const uint32_t *__restrict__ samp, uint4 *__restrict__ bnd) {
-    const uint32_t sid = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t g = sid / G.spg, w = sid % G.spg, spr = G.r / M4_S;  // samples per full run
-    if (g >= G.ngroups) return;
-    const uint32_t k = w / spr, q = w % spr;
-    uint32_t len[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) len[j] = m4_run_len(G, g, (uint32_t)j);
-    if ((uint64_t)q * M4_S >= len[k]) return;  // past a short last run
-    const uint32_t *gb = src + (size_t)g * 4u * G.r;
-    const uint32_t x = samp[sid];
-    // samples of the other runs that precede (x, k) in (key, run) order: upper bound in the
-    // runs before k, lower bound in the runs after it.  The three searches run interleaved,
-    // branch-free, one probe of each per step, so the thread waits on one chain of
-    // log2(r / M4_S) dependent loads instead of three in a row.
-    const uint32_t xf = x ^ flip;
-    uint32_t cnt[4], ns[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        cnt[j] = 0u;
-        ns[j] = (uint32_t)j == k ? 0u : (len[j] + M4_S - 1) / M4_S;
-    }
-    for (uint32_t step = 1u << (31 - __builtin_clz(spr)); step; step >>= 1) {
-        uint32_t v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t p = cnt[j] + step;
-            v[j] = p <= ns[j] ? samp[(size_t)g * G.spg + (size_t)j * spr + p - 1u] ^ flip : 0xFFFFFFFFu;
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t p = cnt[j] + step;
-            const bool le = (uint32_t)j < k;
-            if (p <= ns[j] && (v[j] < xf || (le && v[j] == xf))) cnt[j] = p;
-        }
-    }
+constexpr uint32_t M4_RB = 256;                // threads per rank workgroup
+constexpr uint32_t M4_RSPT = 2;                // samples per thread
+constexpr uint32_t M4_RT = M4_RB * M4_RSPT;    // samples per rank workgroup
+constexpr uint32_t M4_RW = 1024;               // most samples of another run held in LDS per workgroup
+
+// a boundary sample (merged index m, a multiple of M4_M): its cut in every run -- in run j
+// between the last preceding sample and the next, so within one sample gap (a binary search:
+// 16 independent probes every 8 keys and then 7 around the crossing took the rank kernel from
+// 0.075 to 0.149 ms per pass, r29)
+__device__ __forceinline__ void m4_write_cut(const uint32_t *src, const M4Geo &G, uint32_t flip, uint32_t g, uint32_t k,
+                                             uint32_t q, uint32_t x, const uint32_t (&cnt)[4], const uint32_t (&len)[4],
+                                             uint4 *bnd) {
     const uint32_t m = q + cnt[0] + cnt[1] + cnt[2] + cnt[3];
     if (m == 0u || m % M4_M != 0u) return;
-    // a boundary: its cut in every run -- in run j between the last preceding sample and the
-    // next, so within one sample gap (one in M4_M threads gets here; an interleaved
-    // branch-free form of these three searches stopped at the gap's start on the device when
-    // every sample of the run preceded, r29)
+    const uint32_t *gb = src + (size_t)g * 4u * G.r;
     uint32_t cut[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        if ((uint32_t)j == k) {
-            cut[j] = q * M4_S;
-            continue;
-        }
-        if (!len[j]) {
-            cut[j] = 0u;
-            continue;
-        }
         const uint32_t lo = cnt[j] ? (cnt[j] - 1u) * M4_S + 1u : 0u;
         const uint32_t hi = cnt[j] * M4_S < len[j] ? cnt[j] * M4_S : len[j];
-        cut[j] = m4_bound(gb + (size_t)j * G.r, lo, hi, x, (uint32_t)j < k, flip);
+        cut[j] = (uint32_t)j == k ? q * M4_S : m4_bound(gb + (size_t)j * G.r, lo, hi, x, (uint32_t)j < k, flip);
     }
     bnd[(size_t)g * G.bpg + m / M4_M] = make_uint4(cut[0], cut[1], cut[2], cut[3]);
 }
 
-// merge-path co-rank in LDS: A elements among the first d of merge(A, B) (FLIP: int32 order)
+// every sample's merged-order index; boundaries (every M4_M-th) write their cuts.  A
+// workgroup's M4_RT samples are consecutive in one run k (when the run has that many), so
+// each count is monotone over them: six 32-lane groups first count the tile's first and last
+// sample in the three other runs (32-ary searches over the compacted samples: log32(r / M4_S)
+// rounds of loads), the windows of samples between those brackets are loaded into LDS (for
+// uniform keys about M4_RT each), and every thread then searches its samples' brackets in
+// LDS.  r29 at 2^28, per pass: one full binary search per sample and run 0.116 ms (a chain
+// of log2(r / M4_S) scattered L2 loads); this form 0.074-0.078 ms with 1 or 2 samples per
+// thread, 0.101 with 4.
+__global__ __launch_bounds__(M4_RB) void k_m4_rank(const uint32_t *__restrict__ src, M4Geo G, uint32_t flip,
+                                                   const uint32_t *__restrict__ samp, uint4 *__restrict__ bnd) {
+    __shared__ uint32_t win[3][M4_RW];
+    __shared__ uint32_t s_br[6];
+    const uint32_t tid = threadIdx.x, s0 = blockIdx.x * M4_RT, spr = G.r / M4_S;  // samples per full run
+    const uint32_t g = s0 / G.spg, k = (s0 % G.spg) / spr, q0 = (s0 % G.spg) % spr;
+    if (g >= G.ngroups) return;
+    if (q0 + M4_RT > spr) {
+        // runs shorter than a tile: one full search per sample and run (the tile may span
+        // groups: each sample's own group, run and run lengths)
+        for (uint32_t e = 0; e < M4_RSPT; ++e) {
+            const uint32_t sid = s0 + tid + e * M4_RB, w = sid % G.spg, gg = sid / G.spg, kk = w / spr, q = w % spr;
+            if (gg >= G.ngroups) continue;
+            uint32_t len[4], cnt[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) len[j] = m4_run_len(G, gg, (uint32_t)j);
+            if (q >= (len[kk] + M4_S - 1) / M4_S) continue;
+            const uint32_t *ts = samp + (size_t)gg * G.spg;
+            const uint32_t x = ts[(size_t)kk * spr + q];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                cnt[j] = (uint32_t)j == kk ? 0u
+                                           : m4_bound(ts + (size_t)j * spr, 0u, (len[j] + M4_S - 1) / M4_S, x, (uint32_t)j < kk, flip);
+            m4_write_cut(src, G, flip, gg, kk, q, x, cnt, len, bnd);
+        }
+        return;
+    }
+    uint32_t len[4], ns[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        len[j] = m4_run_len(G, g, (uint32_t)j);
+        ns[j] = (len[j] + M4_S - 1) / M4_S;
+    }
+    if (q0 >= ns[k]) return;  // past a short last run: every sample of the tile (uniform)
+    const uint32_t *gs = samp + (size_t)g * G.spg;  // the group's samples, run j at j spr
+    const uint32_t qlast = q0 + M4_RT - 1u < ns[k] - 1u ? q0 + M4_RT - 1u : ns[k] - 1u;
+    if (tid < 192u) {
+        const uint32_t l = tid & 31u, sidx = tid >> 5;  // search 0..5: run i = sidx % 3, first / last sample
+        const uint32_t i = sidx % 3u, j = i + (i >= k);
+        const uint32_t *js = gs + (size_t)j * spr;
+        const uint32_t xf = gs[(size_t)k * spr + (sidx < 3u ? q0 : qlast)] ^ flip;
+        const bool le = j < k;
+        uint32_t lo = 0u, hi = ns[j];  // the count is in [lo, hi]
+        while (lo < hi) {
+            const uint32_t step = (hi - lo + 31u) >> 5;
+            const uint32_t pp = lo + (l + 1u) * step - 1u;  // probe sample pp
+            bool pred = false;
+            if (pp < hi) {
+                const uint32_t v = js[pp] ^ flip;
+                pred = v < xf || (le && v == xf);
+            }
+            const uint64_t bal = __ballot(pred);
+            const uint32_t t = __builtin_popcount((uint32_t)(tid & 32u ? bal >> 32 : bal));
+            const uint32_t nhi = lo + (t + 1u) * step - 1u;
+            hi = nhi < hi ? nhi : hi;
+            lo += t * step;
+        }
+        if (l == 0u) s_br[sidx] = lo;
+    }
+    __syncthreads();
+    uint32_t lo[3], w[3], wmax = 0u;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        lo[i] = s_br[i];
+        w[i] = s_br[i + 3] - s_br[i];
+        wmax = w[i] > wmax ? w[i] : wmax;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const uint32_t j = (uint32_t)i + ((uint32_t)i >= k);
+        if (w[i] <= M4_RW)
+            for (uint32_t e = tid; e < w[i]; e += M4_RB) win[i][e] = gs[(size_t)j * spr + lo[i] + e];
+    }
+    __syncthreads();
+    uint32_t xf[M4_RSPT], c[M4_RSPT][3];
+#pragma unroll
+    for (uint32_t e = 0; e < M4_RSPT; ++e) {
+        const uint32_t q = q0 + tid + e * M4_RB;
+        xf[e] = gs[(size_t)k * spr + (q < ns[k] ? q : qlast)] ^ flip;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) c[e][i] = lo[i];
+    }
+    // the bracketed searches of all the thread's samples and runs interleaved, branch-free
+    for (uint32_t step = wmax ? 1u << (31 - __builtin_clz(wmax)) : 0u; step; step >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const uint32_t j = (uint32_t)i + ((uint32_t)i >= k);
+#pragma unroll
+            for (uint32_t e = 0; e < M4_RSPT; ++e) {
+                const uint32_t p = c[e][i] + step;  // probe sample p - 1
+                const bool in = p <= lo[i] + w[i];
+                const uint32_t v = in ? (w[i] <= M4_RW ? win[i][p - 1u - lo[i]] : gs[(size_t)j * spr + p - 1u]) ^ flip : 0u;
+                if (in && (v < xf[e] || (j < k && v == xf[e]))) c[e][i] = p;
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t e = 0; e < M4_RSPT; ++e) {
+        const uint32_t q = q0 + tid + e * M4_RB;
+        if (q >= ns[k]) continue;
+        uint32_t cnt[4];
+        cnt[k] = 0u;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) cnt[i + (i >= (int)k)] = c[e][i];
+        m4_write_cut(src, G, flip, g, k, q, xf[e] ^ flip, cnt, len, bnd);
+    }
+}
+
+// merge-path co-rank in LDS: A elements among the first d of merge(A, B) (FLIP: int32 order).
+// r29, measured slower: a branch-free form with a workgroup-uniform number of halving steps
+// (7 VALU per step instead of 9; +0.09 ms per pass: the data-dependent loop stops early), and
+// two-step searches (the co-ranks of every 64th diagonal first, by two waves, then each thread
+// within its 64: +0.10 ms per pass from the two extra barriers per block)
 template <bool FLIP>
 __device__ __forceinline__ uint32_t m4_corank(const uint32_t *A, uint32_t la, const uint32_t *B, uint32_t lb, uint32_t d) {
     constexpr uint32_t flip = FLIP ? 0x80000000u : 0u;
@@ -158,8 +242,8 @@ __device__ __forceinline__ uint32_t m4_corank(const uint32_t *A, uint32_t la, co
 }
 
 // 8 consecutive LDS words base[i .. i + 8) by five 8-B reads of the 10 words from i rounded
-// down to even, and one select per word (the pass is VALU-bound: r29 counters; 16-B reads
-// needed three selects per word, 4-B reads hit the lanes' shared banks 4 ways)
+// down to even, and one select per word (16-B reads needed three selects per word; eight 4-B
+// reads, no selects: 0.691 vs 0.687 ms per pass, r29)
 __device__ __forceinline__ void m4_read8(const uint32_t *base, uint32_t i, uint32_t (&w)[M4_KPT]) {
     const uint32_t a = i & ~1u;
     const bool odd = (i & 1u) != 0u;
@@ -210,10 +294,12 @@ __device__ __forceinline__ void m4_window_merge(const uint32_t *buf, uint32_t A,
 }
 
 constexpr uint32_t M4_PAD = M4_KPT;  // +inf words after every run in LDS
+// buf[p]: a block's keys A | pad | B | pad | C | pad | D | pad, then its output staging;
+// buf[1 - p]: level 1's A+B | pad | C+D | pad, then the next block's keys (p alternates)
+constexpr uint32_t M4_BUFW = M4_CAP + 4 * M4_PAD + 16;
 struct alignas(16) M4Smem {
-    alignas(16) uint32_t in[M4_CAP + 4 * M4_PAD + 16];  // A | pad | B | pad | C | pad | D | pad; then the output staging
-    alignas(16) uint32_t mid[M4_CAP + 4 * M4_PAD + 16]; // level 1: A+B | pad | C+D | pad
-    uint4 lo[M4_MAX_PER + 1];                           // each of the workgroup's blocks' start cuts (read once, at entry)
+    alignas(16) uint32_t buf[2][M4_BUFW];
+    uint4 lo[M4_MAX_PER + 1];  // each of the workgroup's blocks' start cuts (read once, at entry)
 };
 
 struct M4Blk {
@@ -257,12 +343,10 @@ __device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *lo, uint3
     return q;
 }
 
-// LABSORT_M4_DIAG (timing builds only, wrong output): 1 = level 1 skipped, 2 = level 2
-// skipped (level 1's result stored), 3 = co-rank searches replaced by d / 2
-#ifndef LABSORT_M4_DIAG
-#define LABSORT_M4_DIAG 0
-#endif
-// workgroup: blocks [b0, b1) of the flat list in turn
+// workgroup: blocks [b0, b1) of the flat list in turn.  Two LDS buffers alternate roles, so
+// a block takes three barriers: keys in X -> level 1 into Y -> level 2 back into X (staging)
+// -> the stores read X while the next block's keys go into Y, which becomes its X (r29: four
+// barriers with fixed in / mid / staging roles, 0.685 ms per pass at 2^28)
 template <bool FLIP>
 __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                           M4Geo G, const uint4 *__restrict__ bnd, uint32_t per,
@@ -273,22 +357,35 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
     const uint32_t b0 = blockIdx.x * per;
     if (b0 >= G.nblocks) return;
     const uint32_t b1 = b0 + per < G.nblocks ? b0 + per : G.nblocks;
-    // keys of block q into registers: element tid + j BLOCK of the windows A | B | C | D.
-    // (Each window's source address is a running select over the four, not an index into
-    // q.lo[]: a dynamic index put the four bases on the scratch stack, one scratch load per key.)
+    // keys of block q into registers: element tid + j BLOCK of the windows A | B | C | D, at a
+    // 32-bit offset from the group's base (one select of a uniform delta per window boundary,
+    // a saddr load); elements past the block carry +inf (they become D's pads in LDS)
     auto load = [&](const M4Blk &q, uint32_t (&v)[M4_KPT]) {
         const uint32_t o1 = q.len[0], o2 = o1 + q.len[1], o3 = o2 + q.len[2];
-        const uint32_t *gb = src + (size_t)q.g * 4u * G.r;
-        const uint32_t *b0 = gb + q.lo[0], *b1 = gb + G.r + q.lo[1] - o1, *b2 = gb + 2u * G.r + q.lo[2] - o2,
-                       *b3 = gb + 3u * G.r + q.lo[3] - o3;
+        const char *gb = reinterpret_cast<const char *>(src + (size_t)q.g * 4u * G.r);
+        const uint32_t d0 = q.lo[0], d1 = G.r + q.lo[1] - o1, d2 = 2u * G.r + q.lo[2] - o2, d3 = 3u * G.r + q.lo[3] - o3;
 #pragma unroll
         for (int j = 0; j < M4_KPT; ++j) {
             const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
-            const uint32_t *a = b0;
-            a = i >= o1 ? b1 : a;
-            a = i >= o2 ? b2 : a;
-            a = i >= o3 ? b3 : a;
-            v[j] = i < q.tot ? ld_stream<NT_MERGE>(a + i) : 0u;
+            uint32_t dd = d0;
+            dd = i >= o1 ? d1 : dd;
+            dd = i >= o2 ? d2 : dd;
+            dd = i >= o3 ? d3 : dd;
+            v[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(gb + (uint32_t)((i + dd) * 4u))) : PADV;
+        }
+    };
+    // block q's keys (registers v) into X with a pad of +inf after each window
+    auto put = [&](uint32_t *X, const M4Blk &q, const uint32_t (&v)[M4_KPT]) {
+        const uint32_t la = q.len[0], lab = la + q.len[1], labc = lab + q.len[2];
+#pragma unroll
+        for (int j = 0; j < M4_KPT; ++j) {
+            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
+            const uint32_t sh = (i >= la ? M4_PAD : 0u) + (i >= lab ? M4_PAD : 0u) + (i >= labc ? M4_PAD : 0u);
+            X[i + sh] = v[j];  // (past the block: +inf, D's pads first)
+        }
+        if (tid < 3u * M4_PAD) {  // A's, B's and C's pads
+            const uint32_t k = tid / M4_PAD, e = tid % M4_PAD;
+            X[(k == 0 ? la : k == 1 ? lab + M4_PAD : labc + 2u * M4_PAD) + e] = PADV;
         }
     };
     // the start cuts of blocks b0 .. b1 (a group's first block starts at 0) into LDS: one
@@ -301,62 +398,53 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
     uint32_t nx[M4_KPT];
     M4Blk cur = m4_block(G, sm.lo, b0, 0u);
     load(cur, nx);
+    put(sm.buf[0], cur, nx);
+    M4Blk nxt = cur;
+    if (b0 + 1u < b1) {
+        nxt = m4_block(G, sm.lo, b0 + 1u, 1u);
+        load(nxt, nx);
+    }
+    uint32_t p = 0u;
     for (uint32_t id = b0; id < b1; ++id) {
+        uint32_t *X = sm.buf[p], *Y = sm.buf[p ^ 1u];
         const uint32_t la = cur.len[0], lb = cur.len[1], lc = cur.len[2], ld = cur.len[3];
         const uint32_t oB = la + M4_PAD, oC = oB + lb + M4_PAD, oD = oC + lc + M4_PAD;  // LDS offsets (A at 0)
-        __syncthreads();  // the previous block's output staging (sm.in) has been stored
-#pragma unroll
-        for (int j = 0; j < M4_KPT; ++j) {
-            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
-            const uint32_t k = (i >= la) + (i >= la + lb) + (i >= la + lb + lc);  // window of element i
-            if (i < cur.tot) sm.in[i + k * M4_PAD] = nx[j];
-        }
-        if (tid < 4u * M4_PAD) {  // the pads
-            const uint32_t k = tid / M4_PAD, e = tid % M4_PAD;
-            const uint32_t end = k == 0 ? la : k == 1 ? oB + lb : k == 2 ? oC + lc : oD + ld;
-            sm.in[end + e] = PADV;
-        }
-        M4Blk nxt = cur;
-        if (id + 1u < b1) {
-            nxt = m4_block(G, sm.lo, id + 1u, id + 1u - b0);
-            load(nxt, nx);
-        }
-        __syncthreads();  // sm.in holds the block
         const uint32_t lab = la + lb, lcd = lc + ld, nab = (lab + M4_KPT - 1) / M4_KPT, ncd = (lcd + M4_KPT - 1) / M4_KPT;
-        const uint32_t cdo = nab * M4_KPT + M4_PAD;  // C+D's offset in sm.mid
-        // level 1: A+B (threads < nab) and C+D
+        const uint32_t cdo = nab * M4_KPT + M4_PAD;  // C+D's offset in Y
+        __syncthreads();  // X holds the block; the previous block's stores (from Y) are done
+        // level 1: A+B (threads < nab) and C+D, X -> Y
         {
             const bool ab = tid < nab;
             const uint32_t d = (ab ? tid : tid - nab) * M4_KPT;
             const uint32_t oX = ab ? 0u : oC, oY = ab ? oB : oD;
             const uint32_t l1 = ab ? la : lc, l2 = ab ? lb : ld;
-            if (LABSORT_M4_DIAG != 1 && d < l1 + l2) {
-                const uint32_t ai = LABSORT_M4_DIAG == 3 ? min(d / 2, l1) : m4_corank<FLIP>(sm.in + oX, l1, sm.in + oY, l2, d);
+            if (d < l1 + l2) {
+                const uint32_t ai = m4_corank<FLIP>(X + oX, l1, X + oY, l2, d);
                 uint32_t r[M4_KPT];
-                m4_window_merge<FLIP>(sm.in, oX, ai, oY, d - ai, r);
-                uint32_t *o = sm.mid + (ab ? 0u : cdo) + d;
+                m4_window_merge<FLIP>(X, oX, ai, oY, d - ai, r);
+                uint32_t *o = Y + (ab ? 0u : cdo) + d;
 #pragma unroll
                 for (int j = 0; j < M4_KPT; j += 4)
                     *reinterpret_cast<uint4 *>(o + j) = make_uint4(r[j], r[j + 1], r[j + 2], r[j + 3]);
             }
             if (tid < 2u * M4_PAD)  // pads after A+B's and C+D's last 8-word rows
-                sm.mid[(tid < M4_PAD ? nab * M4_KPT : cdo + ncd * M4_KPT) + tid % M4_PAD] = PADV;
+                Y[(tid < M4_PAD ? nab * M4_KPT : cdo + ncd * M4_KPT) + tid % M4_PAD] = PADV;
         }
-        __syncthreads();  // sm.mid holds A+B and C+D; sm.in is free
-        // level 2: (A+B)+(C+D) into the staging buffer (16-B writes at the thread's diagonal)
+        __syncthreads();  // Y holds A+B and C+D; X is free
+        // level 2: (A+B)+(C+D), Y -> X (16-B writes at the thread's diagonal)
         const uint32_t tot = cur.tot, ph = cur.out & 3u;
         {
             const uint32_t d = tid * M4_KPT;
-            if (LABSORT_M4_DIAG != 2 && d < tot) {
-                const uint32_t ai = LABSORT_M4_DIAG == 3 ? min(d / 2, lab) : m4_corank<FLIP>(sm.mid, lab, sm.mid + cdo, lcd, d);
+            if (d < tot) {
+                const uint32_t ai = m4_corank<FLIP>(Y, lab, Y + cdo, lcd, d);
                 uint32_t r[M4_KPT];
-                m4_window_merge<FLIP>(sm.mid, 0u, ai, cdo, d - ai, r);
+                m4_window_merge<FLIP>(Y, 0u, ai, cdo, d - ai, r);
 #pragma unroll
                 for (int j = 0; j < M4_KPT; j += 4)
-                    *reinterpret_cast<uint4 *>(sm.in + d + j) = make_uint4(r[j], r[j + 1], r[j + 2], r[j + 3]);
+                    *reinterpret_cast<uint4 *>(X + d + j) = make_uint4(r[j], r[j + 1], r[j + 2], r[j + 3]);
             }
         }
-        __syncthreads();  // the block's output staged
+        __syncthreads();  // the block's output staged in X; Y is free
         // store: 16-B chunks aligned in the output (staging word = output word - ph), the
         // partial chunks at both ends by words
         const uint32_t nch = (ph + tot + 3u) / 4u;
@@ -366,20 +454,29 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
         for (uint32_t c = tid; c < nch; c += M4_BLOCK) {
             const uint32_t w0 = 4u * c;
             if (w0 >= ph && w0 + 4u <= ph + tot) {
-                const uint32_t *sw = sm.in + (w0 - ph);
+                const uint32_t *sw = X + (w0 - ph);
                 __builtin_nontemporal_store(u32x4{sw[0], sw[1], sw[2], sw[3]}, reinterpret_cast<u32x4 *>(ob + w0));
                 if (samp_out && ((obase + w0) & (M4_S - 1u)) == 0u) samp_out[(obase + w0) / M4_S] = sw[0];
             } else {
 #pragma unroll
                 for (uint32_t e = 0; e < 4u; ++e)
                     if (w0 + e >= ph && w0 + e < ph + tot) {
-                        ob[w0 + e] = sm.in[w0 + e - ph];
+                        ob[w0 + e] = X[w0 + e - ph];
                         if (samp_out && ((obase + w0 + e) & (M4_S - 1u)) == 0u)
-                            samp_out[(obase + w0 + e) / M4_S] = sm.in[w0 + e - ph];
+                            samp_out[(obase + w0 + e) / M4_S] = X[w0 + e - ph];
                     }
             }
         }
-        cur = nxt;
+        // the next block's keys into Y (its X), and the one after into registers
+        if (id + 1u < b1) {
+            put(Y, nxt, nx);
+            cur = nxt;
+            if (id + 2u < b1) {
+                nxt = m4_block(G, sm.lo, id + 2u, id + 2u - b0);
+                load(nxt, nx);
+            }
+        }
+        p ^= 1u;
     }
 }
 
@@ -422,7 +519,7 @@ hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_
         k_m4_sample<<<(unsigned)((nsamp + 255) / 256), 256, 0, s>>>(in, G, own);
         samp = own;
     }
-    k_m4_rank<<<(unsigned)((nsamp + 255) / 256), 256, 0, s>>>(in, G, flip, samp, reinterpret_cast<uint4 *>(bnd));
+    k_m4_rank<<<(unsigned)((nsamp + M4_RT - 1) / M4_RT), M4_RB, 0, s>>>(in, G, flip, samp, reinterpret_cast<uint4 *>(bnd));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     int dev = 0, cus = 0;
