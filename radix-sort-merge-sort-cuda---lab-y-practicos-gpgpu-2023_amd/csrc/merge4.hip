@@ -88,22 +88,62 @@ constexpr uint32_t M4_RT = M4_RB * M4_RSPT;    // samples per rank workgroup
 constexpr uint32_t M4_RW = 1024;               // most samples of another run held in LDS per workgroup
 
 // a boundary sample (merged index m, a multiple of M4_M): its cut in every run -- in run j
-// between the last preceding sample and the next, so within one sample gap (a binary search:
-// 16 independent probes every 8 keys and then 7 around the crossing took the rank kernel from
-// 0.075 to 0.149 ms per pass, r29)
+// between the last preceding sample and the next, so within one sample gap.  The other three
+// runs are searched together, 8-ary: each round loads 7 probes of every run at once and
+// narrows each gap 8-fold, so the < M4_S keys of a gap take 3 rounds of loads.  (r29, per pass
+// at 2^28: one binary search per run in turn, 21 dependent HBM loads, left the rank kernel at
+// 0.075 ms, 0.047 without any cut; 16 + 7 probes per run written with conditional loads,
+// which the compiler serialised, 0.149 ms.)
 __device__ __forceinline__ void m4_write_cut(const uint32_t *src, const M4Geo &G, uint32_t flip, uint32_t g, uint32_t k,
                                              uint32_t q, uint32_t x, const uint32_t (&cnt)[4], const uint32_t (&len)[4],
                                              uint4 *bnd) {
+    static_assert(M4_S <= 8 * 8 * 8, "three 8-ary rounds cover a sample gap");
     const uint32_t m = q + cnt[0] + cnt[1] + cnt[2] + cnt[3];
     if (m == 0u || m % M4_M != 0u) return;
     const uint32_t *gb = src + (size_t)g * 4u * G.r;
+    const uint32_t xf = x ^ flip;
+    const uint32_t *run[3];
+    uint32_t lo[3], hi[3];  // the cut (keys of the run preceding x) is in [lo, hi]
+    bool le[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        const uint32_t j = (uint32_t)i + ((uint32_t)i >= k);
+        run[i] = len[j] ? gb + (size_t)j * G.r : src;  // (an empty run's probes read a valid word, unused)
+        le[i] = j < k;
+        lo[i] = cnt[j] ? (cnt[j] - 1u) * M4_S + 1u : 0u;
+        hi[i] = cnt[j] * M4_S < len[j] ? cnt[j] * M4_S : len[j];
+        hi[i] = hi[i] < lo[i] ? lo[i] : hi[i];
+    }
+#pragma unroll
+    for (int round = 0; round < 3; ++round) {
+        uint32_t v[3][7], step[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            step[i] = (hi[i] - lo[i] + 7u) / 8u;
+#pragma unroll
+            for (int p = 0; p < 7; ++p) {  // probe key lo + (p + 1) step - 1, clamped into the run (unused then)
+                const uint32_t idx = lo[i] + (uint32_t)(p + 1) * step[i] - 1u;
+                const uint32_t top = hi[i] ? hi[i] - 1u : 0u;
+                v[i][p] = run[i][idx < top ? idx : top];
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            uint32_t t = 0u;
+#pragma unroll
+            for (int p = 0; p < 7; ++p) {
+                const uint32_t idx = lo[i] + (uint32_t)(p + 1) * step[i] - 1u, vf = v[i][p] ^ flip;
+                t += (idx < hi[i] && (vf < xf || (le[i] && vf == xf))) ? 1u : 0u;
+            }
+            const uint32_t nhi = lo[i] + (t + 1u) * step[i] - 1u;  // probe t failed (none does when t = 7)
+            hi[i] = step[i] && t < 7u ? (nhi < hi[i] ? nhi : hi[i]) : hi[i];
+            lo[i] += t * step[i];
+        }
+    }
     uint32_t cut[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t lo = cnt[j] ? (cnt[j] - 1u) * M4_S + 1u : 0u;
-        const uint32_t hi = cnt[j] * M4_S < len[j] ? cnt[j] * M4_S : len[j];
-        cut[j] = (uint32_t)j == k ? q * M4_S : m4_bound(gb + (size_t)j * G.r, lo, hi, x, (uint32_t)j < k, flip);
-    }
+    for (int i = 0; i < 3; ++i) cut[i + (i >= (int)k)] = lo[i];
+    cut[k] = q * M4_S;
     bnd[(size_t)g * G.bpg + m / M4_M] = make_uint4(cut[0], cut[1], cut[2], cut[3]);
 }
 
@@ -335,7 +375,8 @@ __device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *lo, uint3
     q.tot = q.len[0] + q.len[1] + q.len[2] + q.len[3];
     // (cannot happen with consistent cuts; a broken table must not send loads or stores out
     // of the runs: the block is skipped and the sort's output check fails instead)
-    if (h4.x < l4.x || h4.y < l4.y || h4.z < l4.z || h4.w < l4.w || q.tot > M4_CAP - 2 * M4_KPT) {
+    if (h4.x < l4.x || h4.y < l4.y || h4.z < l4.z || h4.w < l4.w || h4.x > rl[0] || h4.y > rl[1] || h4.z > rl[2] ||
+        h4.w > rl[3] || q.tot > M4_CAP - 2 * M4_KPT) {
         q.tot = 0u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) q.len[j] = 0u;
