@@ -25,11 +25,12 @@ import os
 import shutil
 import sys
 
-CLASSES = {"k_onesweep": "onesweep", "k_histogram": "histogram", "k_hist_seg": "histogram",
+CLASSES = {"k_onesweep_p<true>": "onesweep_kv", "k_onesweep": "onesweep", "k_histogram": "histogram", "k_hist_seg": "histogram",
            "k_km_blocks": "kmerge_blocks", "k_merge_pass": "merge",
            "k_tile_sort": "tile_sort", "k_merge_part": "partition", "k_merge_ab": "merge_ab",
            "k_count_descents": "count_descents", "k_fill": "fill", "k_final_copy": "final_copy",
-           "k_wave_split": "wave_split", "k_gsweep": "gsweep", "k_gcopy": "gcopy"}
+           "k_wave_split": "wave_split", "k_gsweep": "gsweep", "k_gcopy": "gcopy",
+           "k_m4_merge": "merge4", "k_m4_rank": "merge4_rank"}
 
 
 def klass(name):
@@ -45,25 +46,31 @@ def read_pmc(path, counter):
     acc = {}
     paths = [path] + [p for p in [path.replace(os.sep + "run_counter", "_merge" + os.sep + "run_counter")]
                       if p != path and os.path.exists(p)]
-    rows = [row for p in paths for row in csv.DictReader(open(p))]
-    if True:
-        for row in rows:
-            if row["Counter_Name"] != counter:
-                continue
-            c = klass(row["Kernel_Name"])
-            if c is None:
-                continue
-            a = acc.setdefault(c, [0.0, 0])
-            a[0] += float(row["Counter_Value"])
-            a[1] += 1
+    rows = [row for p in paths for row in csv.DictReader(open(p))
+            if row["Counter_Name"] == counter and klass(row["Kernel_Name"]) is not None]
+    # only each class's full-size launches: the bench's small legs (configs 1 and 2) launch
+    # the same kernels on 2^16-2^20 keys, whose grids are a fraction of the 2^28 ones
+    gmax = {}
+    for row in rows:
+        c = klass(row["Kernel_Name"])
+        gmax[c] = max(gmax.get(c, 0), int(row["Grid_Size"]))
+    for row in rows:
+        c = klass(row["Kernel_Name"])
+        if int(row["Grid_Size"]) * 2 < gmax[c]:
+            continue
+        a = acc.setdefault(c, [0.0, 0])
+        a[0] += float(row["Counter_Value"])
+        a[1] += 1
     return {c: v[0] / v[1] for c, v in acc.items() if v[1]}
 
 
 # access shapes of each kernel class (the instructions in its ISA): read, write
 SHAPES = {"onesweep": ("cal_rd_buf_nt", "cal_wr_buf"),      # buffer_load_dword nt / buffer_store_dword
+          "onesweep_kv": ("cal_rd_buf_nt", "cal_wr_buf"),
           "histogram": ("cal_rd_x4_nt", None),                # global_load_dwordx4 nt (k_hist_seg)
           "merge": ("cal_rd_dword", "cal_wr_x4"),             # global_load_dword / global_store_dwordx4
           "tile_sort": ("cal_rd_dword", "cal_wr_dword"),      # global_load_dword / global_store_dword
+          "merge4": ("cal_rd_dword", "cal_wr_x4"),            # global_load_dword nt / global_store_dwordx4 nt
           "count_descents": ("cal_rd_dword", None),           # global_load_dword (a check: 1 GiB read)
           "fill": (None, "cal_wr_dword")}                     # global_store_dword (a check: 1 GiB written)
 CAL_BYTES = float(1 << 30)  # every calibration kernel moves 2^28 words per launch
@@ -125,8 +132,8 @@ def main():
                              "write_factor": round(fw, 4),
                              "read_bytes": fr * f * 1024, "write_bytes": fw * w * 1024,
                              "hbm_bytes_per_launch": fr * f * 1024 + fw * w * 1024,
-                             "algorithmic_bytes_per_launch": {"onesweep": 8 * n, "histogram": 4 * n,
-                                                              "merge": 8 * n, "tile_sort": 8 * n,
+                             "algorithmic_bytes_per_launch": {"onesweep": 8 * n, "onesweep_kv": 16 * n, "histogram": 4 * n,
+                                                              "merge": 8 * n, "tile_sort": 8 * n, "merge4": 8 * n,
                                                               "count_descents": 4 * n, "fill": 4 * n}.get(c)}
     with open(os.path.join(here, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
