@@ -153,6 +153,26 @@ def test_sort_device_offsets_unaligned(ls, oracle, torch_gpu):
         np.testing.assert_array_equal(from_dev(o)[3:3 + n - 2], oracle.sort_u32(a[1:n - 1]))
 
 
+@pytest.mark.parametrize("n", [(1 << 17), (1 << 17) + 1, 3 * 32768 + 7, (1 << 19) + 32768 * 3 + 5, (1 << 21) - 1,
+                               (1 << 22) + 65536 + 128, (1 << 24) + 5])
+@pytest.mark.parametrize("dist", ["u32", "lowbits2", "sorted", "reversed"])
+def test_merge_four_way_shapes(ls, oracle, torch_gpu, n, dist):
+    """The merge sort's four-way passes (merge4.hip): run counts that leave the last group
+    with one to three runs, short last runs, the first four-way pass over 32768-key runs
+    (the rank kernel's per-sample path: fewer samples per run than a workgroup takes) and
+    later ones (its bracketed path), keys repeated across every run (block cuts inside
+    runs of equal keys), int32 order."""
+    torch = torch_gpu
+    base = "lowbits" if dist == "lowbits2" else dist
+    a = oracle.gen(n, SEED + 40 + n % 997, base, param=2 if dist == "lowbits2" else 0)  # lowbits2: keys 0..3
+    t = to_dev(torch, a)
+    o = torch.empty_like(t)
+    for key in ("u32", "i32"):
+        ls.sort_device(t, o, n, key=key, algo="merge")
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key), err_msg=f"{key}")
+
+
 # ---- merge building blocks ------------------------------------------------------------------
 def test_merge_pass(ls, oracle, torch_gpu):
     torch = torch_gpu
