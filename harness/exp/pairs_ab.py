@@ -29,10 +29,10 @@ ko, vo = torch.empty_like(k), torch.empty_like(v)
 st = torch.cuda.current_stream().cuda_stream
 first = L[libs[0]]
 assert first.labsort_fill(k.data_ptr(), n, 0x5EED0003, 0, 0, 0, p(st)) == 0
-mode = os.environ.get("MODE", "pairs")
+mode = os.environ.get("MODE", "pairs")  # pairs | keys | merge | pairsmerge (key/value merge sort)
 keys = mode in ("keys", "merge")
-algo = 1 if mode == "merge" else 0
-wsb = max((h.labsort_workspace_bytes(n, algo) if keys else h.labsort_pairs_workspace_bytes(n, 0)) for h in L.values())
+algo = 1 if mode in ("merge", "pairsmerge") else 0
+wsb = max((h.labsort_workspace_bytes(n, algo) if keys else h.labsort_pairs_workspace_bytes(n, algo)) for h in L.values())
 ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
 ref = None
 for r in range(reps):
@@ -40,7 +40,7 @@ for r in range(reps):
         if keys:
             call = lambda: h.labsort_sort_device(k.data_ptr(), ko.data_ptr(), n, 0, algo, ws.data_ptr(), wsb, p(st))
         else:
-            call = lambda: h.labsort_sort_pairs_device(k.data_ptr(), v.data_ptr(), ko.data_ptr(), vo.data_ptr(), n, 0, 0,
+            call = lambda: h.labsort_sort_pairs_device(k.data_ptr(), v.data_ptr(), ko.data_ptr(), vo.data_ptr(), n, 0, algo,
                                                        ws.data_ptr(), wsb, p(st))
         for _ in range(3):
             assert call() == 0

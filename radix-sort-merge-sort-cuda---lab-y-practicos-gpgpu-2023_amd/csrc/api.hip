@@ -739,10 +739,44 @@ int labsort_merge_runs(const void *d_in, void *d_out, const size_t *h_offsets, i
 
 size_t labsort_pair_tile_keys(void) { return (size_t)TS_TILE_KV; }
 
+namespace {
+// key/value merge sort: levels above the TS_TILE_KV-pair tiles, and its workspace: the keys'
+// and payloads' ping-pong buffers, then (LABSORT_MERGE4) the four-way passes' boundary
+// tables and the two sample buffers
+int pairs_merge_levels(size_t n) {
+    int m = 0;
+    for (size_t run = TS_TILE_KV; run < n; run *= 2) ++m;
+    return m;
+}
+struct PairsMergeLayout {
+    size_t off_tk, off_tv, off_bnd, off_samp[2], total;
+};
+PairsMergeLayout pairs_merge_layout(size_t n) {
+    PairsMergeLayout L{};
+    size_t o = 0;
+    L.off_tk = o;
+    o = align_up(o + n * 4, 256);
+    L.off_tv = o;
+    o = align_up(o + n * 4, 256);
+    L.off_bnd = o;
+    size_t bw = 0;
+    if (LABSORT_MERGE4)
+        for (size_t r = (pairs_merge_levels(n) % 2 ? 2 : 1) * (size_t)TS_TILE_KV; r < n; r *= 4)
+            bw = std::max(bw, merge4_bnd_words(n, r));
+    o = align_up(o + bw * 4, 256);
+    for (int i = 0; i < 2; ++i) {
+        L.off_samp[i] = o;
+        if (bw) o = align_up(o + merge4_samp_words(n) * 4, 256);
+    }
+    L.total = o;
+    return L;
+}
+}  // namespace
+
 size_t labsort_pairs_workspace_bytes(size_t n, int algo) {
     if (n <= (size_t)TS_TILE_KV) return 256;
     algo = resolve_pairs_algo(algo, n);
-    if (algo == LABSORT_ALGO_MERGE) return align_up(n * 4, 256) * 2;  // ping-pong keys | payloads
+    if (algo == LABSORT_ALGO_MERGE) return pairs_merge_layout(n).total;  // ping-pong keys | payloads | four-way tables
     // radix workspace | payload ping-pong
     return align_up(radix_layout(n, 8, OSP_TILE).total, 256) + align_up(n * 4, 256);
 }
@@ -812,25 +846,44 @@ int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void
         return LABSORT_OK;
     }
     if (algo == LABSORT_ALGO_RADIX) return sort_pairs_radix(ki, vi, ko, vo, n, flip, static_cast<char *>(d_ws), s);
-    // merge passes over runs of TS_TILE_KV pairs, ping-pong between out and the workspace;
-    // the tile sort writes where the pass count makes the last pass land in out
-    uint32_t *tk = static_cast<uint32_t *>(d_ws);
-    uint32_t *tv = reinterpret_cast<uint32_t *>(static_cast<char *>(d_ws) + align_up(n * 4, 256));
-    int m = 0;
-    for (size_t run = TS_TILE_KV; run < n; run *= 2) ++m;
-    uint32_t *ck = (m % 2 == 0) ? ko : tk, *cv = (m % 2 == 0) ? vo : tv;
+    // merge passes over runs of TS_TILE_KV pairs, ping-pong between out and the workspace:
+    // four-way passes carrying the payloads (k_m4_merge_kv) and, for an odd level count,
+    // one pairwise pass first (as sort_merge); the tile sort writes where the pass count
+    // makes the last pass land in out
+    const PairsMergeLayout L = pairs_merge_layout(n);
+    char *ws = static_cast<char *>(d_ws);
+    uint32_t *tk = reinterpret_cast<uint32_t *>(ws + L.off_tk), *tv = reinterpret_cast<uint32_t *>(ws + L.off_tv);
+    uint32_t *bnd = reinterpret_cast<uint32_t *>(ws + L.off_bnd);
+    uint32_t *samp[2] = {reinterpret_cast<uint32_t *>(ws + L.off_samp[0]), reinterpret_cast<uint32_t *>(ws + L.off_samp[1])};
+    const int m = pairs_merge_levels(n);
+    const bool four = LABSORT_MERGE4 && (((uintptr_t)ko | (uintptr_t)vo | (uintptr_t)tk | (uintptr_t)tv) & 15u) == 0;
+    const int npass = four ? m / 2 + m % 2 : m;
+    uint32_t *ck = (npass % 2 == 0) ? ko : tk, *cv = (npass % 2 == 0) ? vo : tv;
+    int sb = 0;
+    auto next_is_four = [&](int lv) { return four && lv < m && (m - lv) % 2 == 0; };
     {
         TimingScope ts(LABSORT_K_TILE_SORT, s);
-        HIP_TRY(launch_tile_sort_kv(ki, ck, vi, cv, n, flip, s));
+        HIP_TRY(launch_tile_sort_kv(ki, ck, vi, cv, n, flip, s, next_is_four(0) ? samp[sb] : nullptr));
     }
     size_t run = TS_TILE_KV;
-    for (int k = 0; k < m; ++k) {
+    for (int lv = 0; lv < m;) {
         uint32_t *nk = (ck == ko) ? tk : ko, *nv = (cv == vo) ? tv : vo;
-        TimingScope ts(LABSORT_K_MERGE, s);
-        HIP_TRY(launch_merge_pass(ck, nk, n, run, flip, nullptr, s, cv, nv));
+        if (next_is_four(lv)) {
+            TimingScope ts(LABSORT_K_MERGE4, s);
+            HIP_TRY(launch_merge4_pass(ck, nk, n, run, flip, bnd, samp[sb], next_is_four(lv + 2) ? samp[sb ^ 1] : nullptr,
+                                       s, cv, nv));
+            sb ^= 1;
+            run *= 4;
+            lv += 2;
+        } else {
+            TimingScope ts(LABSORT_K_MERGE, s);
+            HIP_TRY(launch_merge_pass(ck, nk, n, run, flip, nullptr, s, cv, nv, nullptr,
+                                      next_is_four(lv + 1) ? samp[sb] : nullptr));
+            run *= 2;
+            lv += 1;
+        }
         ck = nk;
         cv = nv;
-        run *= 2;
     }
     return LABSORT_OK;
 }

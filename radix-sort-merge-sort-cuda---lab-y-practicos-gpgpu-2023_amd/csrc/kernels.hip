@@ -1587,7 +1587,7 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
             }
             // samp_out: every M4_S-th output key for a four-way pass next (merge4.hip): the
             // wave's 64 KPT outputs hold 64 KPT / M4_S of them, one store by as many lanes
-            if constexpr (!KV) {
+            {
                 static_assert((64 * KPT) % M4_S == 0 && (uint32_t)MG_TILE % M4_S == 0, "samples per wave");
                 if (samp_out && lane < 64u * KPT / M4_S)
                     samp_out[(cur.o0 + w * 64u * KPT) / M4_S + lane] = wo[M4_S * lane];
@@ -1619,7 +1619,7 @@ __global__ __launch_bounds__(BLOCK, KV ? 4 : 8) void k_merge_pass_p(const uint32
             const uint32_t i = tid + (uint32_t)j * BLOCK;
             if (i < tot) {
                 o[i] = sm.out[i + (i >> 5)];
-                if (!KV && samp_out && ((cur.o0 + i) & (M4_S - 1u)) == 0u) samp_out[(cur.o0 + i) / M4_S] = sm.out[i + (i >> 5)];
+                if (samp_out && ((cur.o0 + i) & (M4_S - 1u)) == 0u) samp_out[(cur.o0 + i) / M4_S] = sm.out[i + (i >> 5)];
             }
         }
         if constexpr (KV) {
@@ -1870,7 +1870,7 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
     const uint32_t g = (ntiles + m - 1) / m;
     if (vin)
         k_merge_pass_p<MG_BLOCK, MG_KPT, true>
-            <<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr, vin, vout);
+            <<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr, vin, vout, samp_out);
     else
         k_merge_pass_p<MG_BLOCK, MG_KPT><<<g, MG_BLOCK, 0, s>>>(in, out, (uint32_t)n, (uint32_t)run, flip, ntiles, m, pr,
                                                                 nullptr, nullptr, samp_out);
@@ -1878,10 +1878,10 @@ hipError_t launch_merge_pass(const uint32_t *in, uint32_t *out, size_t n, size_t
 }
 
 hipError_t launch_tile_sort_kv(const uint32_t *in, uint32_t *out, const uint32_t *vin, uint32_t *vout, size_t n,
-                               uint32_t flip, hipStream_t s) {
+                               uint32_t flip, hipStream_t s, uint32_t *samp_out) {
     if (n == 0) return hipSuccess;
     const unsigned g = (unsigned)((n + TS_TILE_KV - 1) / TS_TILE_KV);
-    k_tile_sort<TS_BLOCK, TS_KPT_KV, true><<<g, TS_BLOCK, 0, s>>>(in, out, vin, vout, (uint32_t)n, flip);
+    k_tile_sort<TS_BLOCK, TS_KPT_KV, true><<<g, TS_BLOCK, 0, s>>>(in, out, vin, vout, (uint32_t)n, flip, samp_out);
     return hipGetLastError();
 }
 

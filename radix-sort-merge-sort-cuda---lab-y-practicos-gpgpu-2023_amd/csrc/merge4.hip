@@ -521,6 +521,169 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
     }
 }
 
+// Key/value four-way merge (payloads of 4 bytes; labsort_sort_pairs_device with
+// LABSORT_ALGO_MERGE).  The same blocks, rank and schedule as k_m4_merge, with every key's
+// payload carried beside it through both LDS buffers; each level is the stable merge of the
+// pairwise key/value pass (co-rank, then the thread's 8 outputs taken in turn, "A before
+// equal B" -- lab.cu:163-170 -- each output remembering the LDS slot it came from, the
+// payloads read from those slots afterwards).  The four-way order (key, run, position) and
+// the runs' input order make the merge sort stable, as the pairwise passes were.
+struct alignas(16) M4SmemKV {
+    alignas(16) uint32_t buf[2][M4_BUFW];
+    alignas(16) uint32_t vbuf[2][M4_BUFW];
+    uint4 lo[M4_MAX_PER + 1];
+};
+
+// the thread's 8 outputs at diagonal d of the stable merge of K[oa, oa + la) and
+// K[ob, ob + lb) (keys r, payloads pv from V at the same slots)
+template <bool FLIP>
+__device__ __forceinline__ void m4_merge8_kv(const uint32_t *K, const uint32_t *V, uint32_t oa, uint32_t la, uint32_t ob,
+                                             uint32_t lb, uint32_t d, uint32_t (&r)[M4_KPT], uint32_t (&pv)[M4_KPT]) {
+    constexpr uint32_t flip = FLIP ? 0x80000000u : 0u;
+    uint32_t ai = m4_corank<FLIP>(K + oa, la, K + ob, lb, d), bi = d - ai;
+    uint32_t va = ai < la ? K[oa + ai] : 0u, vb = bi < lb ? K[ob + bi] : 0u;
+    uint32_t from[M4_KPT];
+#pragma unroll
+    for (int j = 0; j < M4_KPT; ++j) {
+        const bool takeA = bi >= lb || (ai < la && (va ^ flip) <= (vb ^ flip));
+        r[j] = takeA ? va : vb;
+        from[j] = takeA ? oa + ai : ob + bi;
+        if (takeA) {
+            ++ai;
+            va = ai < la ? K[oa + ai] : 0u;
+        } else {
+            ++bi;
+            vb = bi < lb ? K[ob + bi] : 0u;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < M4_KPT; ++j) pv[j] = V[from[j]];
+}
+
+template <bool FLIP>
+__global__ __launch_bounds__(M4_BLOCK, 4) void k_m4_merge_kv(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
+                                                             const uint32_t *__restrict__ vsrc, uint32_t *__restrict__ vdst,
+                                                             M4Geo G, const uint4 *__restrict__ bnd, uint32_t per,
+                                                             uint32_t *__restrict__ samp_out) {
+    __shared__ M4SmemKV sm;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b0 = blockIdx.x * per;
+    if (b0 >= G.nblocks) return;
+    const uint32_t b1 = b0 + per < G.nblocks ? b0 + per : G.nblocks;
+    // keys and payloads of block q into registers (as k_m4_merge; no +inf fill: the
+    // key/value merges check their bounds)
+    auto load = [&](const M4Blk &q, uint32_t (&v)[M4_KPT], uint32_t (&pl)[M4_KPT]) {
+        const uint32_t o1 = q.len[0], o2 = o1 + q.len[1], o3 = o2 + q.len[2];
+        const size_t gofs = (size_t)q.g * 4u * G.r;
+        const char *gb = reinterpret_cast<const char *>(src + gofs), *vb = reinterpret_cast<const char *>(vsrc + gofs);
+        const uint32_t d0 = q.lo[0], d1 = G.r + q.lo[1] - o1, d2 = 2u * G.r + q.lo[2] - o2, d3 = 3u * G.r + q.lo[3] - o3;
+#pragma unroll
+        for (int j = 0; j < M4_KPT; ++j) {
+            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
+            uint32_t dd = d0;
+            dd = i >= o1 ? d1 : dd;
+            dd = i >= o2 ? d2 : dd;
+            dd = i >= o3 ? d3 : dd;
+            const uint32_t off = (i + dd) * 4u;
+            v[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(gb + off)) : 0u;
+            pl[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(vb + off)) : 0u;
+        }
+    };
+    auto put = [&](uint32_t *X, uint32_t *XV, const M4Blk &q, const uint32_t (&v)[M4_KPT], const uint32_t (&pl)[M4_KPT]) {
+        const uint32_t la = q.len[0], lab = la + q.len[1], labc = lab + q.len[2];
+#pragma unroll
+        for (int j = 0; j < M4_KPT; ++j) {
+            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
+            const uint32_t sh = (i >= la ? M4_PAD : 0u) + (i >= lab ? M4_PAD : 0u) + (i >= labc ? M4_PAD : 0u);
+            X[i + sh] = v[j];
+            XV[i + sh] = pl[j];
+        }
+    };
+    for (uint32_t t = tid; t <= b1 - b0; t += M4_BLOCK) {
+        const uint32_t id = b0 + t;
+        sm.lo[t] = (id < G.nblocks && id % G.bpg) ? bnd[id] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    __syncthreads();
+    uint32_t nx[M4_KPT], nv[M4_KPT];
+    M4Blk cur = m4_block(G, sm.lo, b0, 0u);
+    load(cur, nx, nv);
+    put(sm.buf[0], sm.vbuf[0], cur, nx, nv);
+    M4Blk nxt = cur;
+    if (b0 + 1u < b1) {
+        nxt = m4_block(G, sm.lo, b0 + 1u, 1u);
+        load(nxt, nx, nv);
+    }
+    uint32_t p = 0u;
+    for (uint32_t id = b0; id < b1; ++id) {
+        uint32_t *X = sm.buf[p], *Y = sm.buf[p ^ 1u], *XV = sm.vbuf[p], *YV = sm.vbuf[p ^ 1u];
+        const uint32_t la = cur.len[0], lb = cur.len[1], lc = cur.len[2], ld = cur.len[3];
+        const uint32_t oB = la + M4_PAD, oC = oB + lb + M4_PAD, oD = oC + lc + M4_PAD;
+        const uint32_t lab = la + lb, lcd = lc + ld, nab = (lab + M4_KPT - 1) / M4_KPT;
+        const uint32_t cdo = nab * M4_KPT + M4_PAD;
+        __syncthreads();  // X holds the block; the previous block's stores (from Y) are done
+        {
+            const bool ab = tid < nab;
+            const uint32_t d = (ab ? tid : tid - nab) * M4_KPT;
+            const uint32_t oX = ab ? 0u : oC, oY = ab ? oB : oD, l1 = ab ? la : lc, l2 = ab ? lb : ld;
+            if (d < l1 + l2) {
+                uint32_t r[M4_KPT], pv[M4_KPT];
+                m4_merge8_kv<FLIP>(X, XV, oX, l1, oY, l2, d, r, pv);
+                const uint32_t o = (ab ? 0u : cdo) + d;
+#pragma unroll
+                for (int j = 0; j < M4_KPT; j += 4) {
+                    *reinterpret_cast<uint4 *>(Y + o + j) = make_uint4(r[j], r[j + 1], r[j + 2], r[j + 3]);
+                    *reinterpret_cast<uint4 *>(YV + o + j) = make_uint4(pv[j], pv[j + 1], pv[j + 2], pv[j + 3]);
+                }
+            }
+        }
+        __syncthreads();  // Y holds A+B and C+D; X is free
+        const uint32_t tot = cur.tot, ph = cur.out & 3u;
+        {
+            const uint32_t d = tid * M4_KPT;
+            if (d < tot) {
+                uint32_t r[M4_KPT], pv[M4_KPT];
+                m4_merge8_kv<FLIP>(Y, YV, 0u, lab, cdo, lcd, d, r, pv);
+#pragma unroll
+                for (int j = 0; j < M4_KPT; j += 4) {
+                    *reinterpret_cast<uint4 *>(X + d + j) = make_uint4(r[j], r[j + 1], r[j + 2], r[j + 3]);
+                    *reinterpret_cast<uint4 *>(XV + d + j) = make_uint4(pv[j], pv[j + 1], pv[j + 2], pv[j + 3]);
+                }
+            }
+        }
+        __syncthreads();  // the block's output staged in X / XV; Y is free
+        const uint32_t nch = (ph + tot + 3u) / 4u;
+        uint32_t *ob = dst + (cur.out - ph), *vob = vdst + (cur.out - ph);
+        const uint32_t obase = cur.out - ph;
+        for (uint32_t c = tid; c < nch; c += M4_BLOCK) {
+            const uint32_t w0 = 4u * c;
+            if (w0 >= ph && w0 + 4u <= ph + tot) {
+                const uint32_t *sw = X + (w0 - ph), *sv = XV + (w0 - ph);
+                __builtin_nontemporal_store(u32x4{sw[0], sw[1], sw[2], sw[3]}, reinterpret_cast<u32x4 *>(ob + w0));
+                __builtin_nontemporal_store(u32x4{sv[0], sv[1], sv[2], sv[3]}, reinterpret_cast<u32x4 *>(vob + w0));
+                if (samp_out && ((obase + w0) & (M4_S - 1u)) == 0u) samp_out[(obase + w0) / M4_S] = sw[0];
+            } else {
+#pragma unroll
+                for (uint32_t e = 0; e < 4u; ++e)
+                    if (w0 + e >= ph && w0 + e < ph + tot) {
+                        ob[w0 + e] = X[w0 + e - ph];
+                        vob[w0 + e] = XV[w0 + e - ph];
+                        if (samp_out && ((obase + w0 + e) & (M4_S - 1u)) == 0u)
+                            samp_out[(obase + w0 + e) / M4_S] = X[w0 + e - ph];
+                    }
+            }
+        }
+        if (id + 1u < b1) {
+            put(Y, YV, nxt, nx, nv);
+            cur = nxt;
+            if (id + 2u < b1) {
+                nxt = m4_block(G, sm.lo, id + 2u, id + 2u - b0);
+                load(nxt, nx, nv);
+            }
+        }
+        p ^= 1u;
+    }
+}
+
 // geometry of a four-way pass over runs of r keys
 M4Geo m4_geo(size_t n, size_t r) {
     M4Geo G{};
@@ -549,9 +712,11 @@ size_t merge4_bnd_words(size_t n, size_t r) {
 }
 
 hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_t r, uint32_t flip, uint32_t *bnd,
-                              const uint32_t *samp_in, uint32_t *samp_out, hipStream_t s) {
+                              const uint32_t *samp_in, uint32_t *samp_out, hipStream_t s, const uint32_t *vin,
+                              uint32_t *vout) {
     if (n == 0) return hipSuccess;
-    if (r % M4_S || n > 0xFFFFFFFFull - 4 * r) return hipErrorInvalidValue;
+    if (r % M4_S || n > 0xFFFFFFFFull - 4 * r || !vin != !vout) return hipErrorInvalidValue;
+    if ((((uintptr_t)out | (uintptr_t)vout) & 15u) != 0) return hipErrorInvalidValue;  // 16-B stores
     const M4Geo G = m4_geo(n, r);
     const size_t nsamp = (size_t)G.ngroups * G.spg;
     const uint32_t *samp = samp_in;
@@ -570,6 +735,17 @@ hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_
     uint32_t per = (G.nblocks + want - 1) / want;
     if (per > M4_MAX_PER) per = M4_MAX_PER;
     const uint32_t g = (G.nblocks + per - 1) / per;
+    if (vin) {
+        const uint32_t want_kv = (uint32_t)(2 * (cus > 0 ? cus : 256));  // two 70 KB workgroups per CU
+        uint32_t pkv = (G.nblocks + want_kv - 1) / want_kv;
+        if (pkv > M4_MAX_PER) pkv = M4_MAX_PER;
+        const uint32_t gkv = (G.nblocks + pkv - 1) / pkv;
+        if (flip)
+            k_m4_merge_kv<true><<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, reinterpret_cast<const uint4 *>(bnd), pkv, samp_out);
+        else
+            k_m4_merge_kv<false><<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, reinterpret_cast<const uint4 *>(bnd), pkv, samp_out);
+        return hipGetLastError();
+    }
     if (flip)
         k_m4_merge<true><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out);
     else

@@ -278,18 +278,21 @@ def test_sort_pairs(ls, oracle, torch_gpu, n, dist, key, algo):
     np.testing.assert_array_equal(from_dev(tv), ev)
 
 
-@pytest.mark.parametrize("dist", ["u32", "sorted", "reversed"])
-def test_sort_pairs_large(ls, oracle, torch_gpu, dist):
-    """Key/value radix at 2^24 + 5 pairs: the persistent onesweep passes (segmented
-    look-back chains, partial first tiles per segment) carrying the payloads."""
+@pytest.mark.parametrize("algo", ["radix", "merge"])
+@pytest.mark.parametrize("dist", ["u32", "sorted", "reversed", "lowbits"])
+def test_sort_pairs_large(ls, oracle, torch_gpu, dist, algo):
+    """Key/value at 2^24 + 5 pairs. radix: the persistent onesweep passes (segmented
+    look-back chains, partial first tiles per segment) carrying the payloads; merge: the
+    key/value four-way passes (k_m4_merge_kv; lowbits: 32 distinct keys, so block cuts fall
+    inside long runs of equal keys and stability is what decides the payload order)."""
     torch = torch_gpu
     n = (1 << 24) + 5
-    k = oracle.gen(n, SEED + 31, dist)
+    k = oracle.gen(n, SEED + 31, dist, param=5 if dist == "lowbits" else 0)
     v = np.arange(n, dtype=np.uint32)
     ek, ev = oracle.stable_sort_pairs(k, v, "u32")
     tk, tv = to_dev(torch, k), to_dev(torch, v)
     ok, ov = torch.empty_like(tk), torch.empty_like(tv)
-    ls.sort_pairs_device(tk, tv, ok, ov, n, key="u32", algo="radix")
+    ls.sort_pairs_device(tk, tv, ok, ov, n, key="u32", algo=algo)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(from_dev(ok), ek)
     np.testing.assert_array_equal(from_dev(ov), ev)
