@@ -736,44 +736,55 @@ def main():
         vin = torch.arange(n, dtype=torch.int32, device=dev)
         pko = torch.empty_like(src)
         pvo = torch.empty_like(src)
-        pws = torch.empty(max(ls.pairs_workspace_bytes(n, "radix"), 256), dtype=torch.uint8, device=dev)
 
-        def pstep():
-            ls.sort_pairs_device(src, vin, pko, pvo, n, key=key, algo="radix", workspace=pws, stream=stream)
+        def prun(palgo, cls):
+            """time args.steps key/value sorts with `palgo`; verify; (ms per step, cls launch mean)"""
+            pws = torch.empty(max(ls.pairs_workspace_bytes(n, palgo), 256), dtype=torch.uint8, device=dev)
 
-        for _ in range(args.warmup):
-            pstep()
-        torch.cuda.synchronize()
-        ls.timing_enable(True)
-        p0 = time.perf_counter()
-        for _ in range(args.steps):
-            pstep()
-        torch.cuda.synchronize()
-        p1 = time.perf_counter()
-        pp_ms, pp_cnt = ls.timing_read("onesweep")
-        ls.timing_enable(False)
-        ls.pairs_workspace_status(pws, n, "radix", stream=stream)
-        pok, _ = verify(torch, ls, src, pko, n, key)
-        if pok:
-            idx = pvo.to(torch.int64)
-            pok = bool((idx >= 0).all()) and bool((idx < n).all()) and torch.equal(src[idx], pko)
-            if pok and n > 1:
-                pok = bool(((pvo[1:] > pvo[:-1]) | (pko[1:] != pko[:-1])).all())
-            del idx
-        if not pok:
-            print("bench.py: KEY/VALUE OUTPUT CHECK FAILED", file=sys.stderr)
-            sys.exit(3)
-        pavg = pp_ms / pp_cnt if pp_cnt else None
+            def pstep():
+                ls.sort_pairs_device(src, vin, pko, pvo, n, key=key, algo=palgo, workspace=pws, stream=stream)
+
+            for _ in range(args.warmup):
+                pstep()
+            torch.cuda.synchronize()
+            ls.timing_enable(True)
+            p0 = time.perf_counter()
+            for _ in range(args.steps):
+                pstep()
+            torch.cuda.synchronize()
+            p1 = time.perf_counter()
+            c_ms, c_cnt = ls.timing_read(cls)
+            ls.timing_enable(False)
+            ls.pairs_workspace_status(pws, n, palgo, stream=stream)
+            del pws
+            pok, _ = verify(torch, ls, src, pko, n, key)
+            if pok:
+                idx = pvo.to(torch.int64)
+                pok = bool((idx >= 0).all()) and bool((idx < n).all()) and torch.equal(src[idx], pko)
+                if pok and n > 1:
+                    pok = bool(((pvo[1:] > pvo[:-1]) | (pko[1:] != pko[:-1])).all())
+                del idx
+            if not pok:
+                print(f"bench.py: KEY/VALUE OUTPUT CHECK FAILED ({palgo})", file=sys.stderr)
+                sys.exit(3)
+            return (p1 - p0) / args.steps * 1e3, (c_ms / c_cnt if c_cnt else None)
+
+        pms, pavg = prun("radix", "onesweep")
+        mms, mavg = prun("merge", "merge4")
         pairs_leg = {"workload": f"stable key/value LSD radix (4-byte payloads) of the same 2^{args.log2n} keys",
-                     "value": round(n * args.steps / (p1 - p0) / 1e6, 2), "unit": "Mpairs/s",
-                     "ms_per_step": round((p1 - p0) / args.steps * 1e3, 4),
+                     "value": round(n / (pms * 1e-3) / 1e6, 2), "unit": "Mpairs/s",
+                     "ms_per_step": round(pms, 4),
                      "verified": "sorted, payload = input index of its key, equal keys in input order",
                      "roofline": {"bound": "hbm", "kernel": "k_onesweep_p<true> (key/value)", "peak": HBM_PEAK_GBS,
                                   "unit": "GB/s", "avg_launch_ms": round(pavg, 5) if pavg else None,
                                   "achieved": round(16.0 * n / (pavg * 1e-3) / 1e9, 1) if pavg else None,
                                   "frac": round(16.0 * n / (pavg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if pavg else None,
-                                  "algorithmic_bytes_per_launch": 16.0 * n}}
-        del vin, pko, pvo, pws
+                                  "algorithmic_bytes_per_launch": 16.0 * n},
+                     "merge": {"workload": "stable key/value merge sort (tile sort + four-way passes carrying the payloads)",
+                               "value": round(n / (mms * 1e-3) / 1e6, 2), "unit": "Mpairs/s", "ms_per_step": round(mms, 4),
+                               "four_way_pass_ms": round(mavg, 5) if mavg else None,
+                               "verified": "sorted, payload = input index of its key, equal keys in input order"}}
+        del vin, pko, pvo
 
     config1 = None
     if args.algo == "radix" and not args.no_merge:
