@@ -110,6 +110,19 @@ def test_radix_workspace_monotone(ls):
     assert ws == sorted(ws), list(zip(edge, ws))
 
 
+def test_merge_workspace_monotone(ls):
+    """The merge workspaces (keys and key/value: ping-pong buffers + the four-way passes'
+    boundary tables and samples) never shrink as n grows, across the level-count edges
+    where the pass schedule changes (an odd level count adds a pairwise pass first)"""
+    T, TK = ls.tile_keys(), ls.pair_tile_keys()
+    edge = sorted({(t << k) + d for t in (T, TK) for k in range(0, 16) for d in (-1, 0, 1, 777)})
+    for name, f in (("merge", lambda n: ls.workspace_bytes(n, "merge")),
+                    ("pairs merge", lambda n: ls.pairs_workspace_bytes(n, "merge"))):
+        ws = [f(n) for n in edge]
+        assert ws == sorted(ws), name
+        assert all(w >= 4 * n for n, w in zip(edge, ws) if n > T), name
+
+
 def test_argument_errors(ls):
     L = ls.lib
     ws = ctypes.create_string_buffer(1 << 16)
