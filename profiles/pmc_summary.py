@@ -25,7 +25,8 @@ import os
 import shutil
 import sys
 
-CLASSES = {"k_onesweep_p<true>": "onesweep_kv", "k_onesweep": "onesweep", "k_histogram": "histogram", "k_hist_seg": "histogram",
+CLASSES = {"k_onesweep_p<true>": "onesweep_kv", "k_m4_merge_kv": "merge4_kv", "k_tile_sort<1024, 16, true>": "tile_sort_kv",
+           "k_onesweep": "onesweep", "k_histogram": "histogram", "k_hist_seg": "histogram",
            "k_km_blocks": "kmerge_blocks", "k_merge_pass": "merge",
            "k_tile_sort": "tile_sort", "k_merge_part": "partition", "k_merge_ab": "merge_ab",
            "k_count_descents": "count_descents", "k_fill": "fill", "k_final_copy": "final_copy",
@@ -71,6 +72,8 @@ SHAPES = {"onesweep": ("cal_rd_buf_nt", "cal_wr_buf"),      # buffer_load_dword 
           "merge": ("cal_rd_dword", "cal_wr_x4"),             # global_load_dword / global_store_dwordx4
           "tile_sort": ("cal_rd_dword", "cal_wr_dword"),      # global_load_dword / global_store_dword
           "merge4": ("cal_rd_dword", "cal_wr_x4"),            # global_load_dword nt / global_store_dwordx4 nt
+          "merge4_kv": ("cal_rd_dword", "cal_wr_x4"),
+          "tile_sort_kv": ("cal_rd_dword", "cal_wr_dword"),
           "count_descents": ("cal_rd_dword", None),           # global_load_dword (a check: 1 GiB read)
           "fill": (None, "cal_wr_dword")}                     # global_store_dword (a check: 1 GiB written)
 CAL_BYTES = float(1 << 30)  # every calibration kernel moves 2^28 words per launch
@@ -134,6 +137,7 @@ def main():
                              "hbm_bytes_per_launch": fr * f * 1024 + fw * w * 1024,
                              "algorithmic_bytes_per_launch": {"onesweep": 8 * n, "onesweep_kv": 16 * n, "histogram": 4 * n,
                                                               "merge": 8 * n, "tile_sort": 8 * n, "merge4": 8 * n,
+                                                              "merge4_kv": 16 * n, "tile_sort_kv": 16 * n,
                                                               "count_descents": 4 * n, "fill": 4 * n}.get(c)}
     with open(os.path.join(here, f"{tag}_pmc.json"), "w") as f:
         json.dump(out, f, indent=1)
