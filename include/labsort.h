@@ -109,11 +109,12 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
 int labsort_sort_host(void *h_keys, size_t n, int key_type, int algo);
 /* Device-side status of the last labsort_sort_device(n, algo) that used d_workspace:
  * synchronises `stream`, then returns LABSORT_ERR_DEVICE if a kernel of that sort set
- * the workspace's error word (a bounded look-back spin expired: the result is not
- * valid), else LABSORT_OK.  The error word is the first 32-bit word of a radix
- * workspace, cleared at the start of every radix sort; merge-path sorts have none and
- * report LABSORT_OK.  The reference's policy (CUDA_CHK after every launch, utils.h:18-26)
- * checks launch status only; this adds the kernels' own failure report. */
+ * the workspace's error word (radix: a bounded look-back spin expired; merge: a four-way
+ * block whose cuts were inconsistent was skipped -- the result is not valid), else
+ * LABSORT_OK.  The error word is the first 32-bit word of the workspace, cleared at the
+ * start of every sort longer than one tile (one tile: no error word, LABSORT_OK).  The
+ * reference's policy (CUDA_CHK after every launch, utils.h:18-26) checks launch status
+ * only; this adds the kernels' own failure report. */
 int labsort_workspace_status(const void *d_workspace, size_t n, int algo, void *stream);
 /* The same for the last labsort_sort_pairs_device(n, algo) on d_workspace. */
 int labsort_pairs_workspace_status(const void *d_workspace, size_t n, int algo, void *stream);

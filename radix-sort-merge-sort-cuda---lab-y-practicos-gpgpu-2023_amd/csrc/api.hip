@@ -142,12 +142,16 @@ int merge_levels(size_t n) {
     return m;
 }
 
+// the error word first (labsort_workspace_status reads the workspace's first word, as for
+// the radix layout), then the ping-pong keys, ...
 struct MergeLayout {
-    size_t off_tmp, off_part, off_bnd, off_samp[2], total;
+    size_t off_err, off_tmp, off_part, off_bnd, off_samp[2], total;
 };
 MergeLayout merge_layout(size_t n) {
     MergeLayout L{};
     size_t o = 0;
+    L.off_err = o;
+    o += 256;
     L.off_tmp = o;
     o = align_up(o + n * 4, 256);
     L.off_part = o;
@@ -256,6 +260,8 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
 // than pairwise passes: 9.7-14 vs 7.9 ms)
 int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s) {
     const MergeLayout L = merge_layout(n);
+    uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
+    HIP_TRY(hipMemsetAsync(err, 0, 4, s));
     uint32_t *tmp = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
     uint32_t *part = reinterpret_cast<uint32_t *>(ws + L.off_part);
     uint32_t *bnd = reinterpret_cast<uint32_t *>(ws + L.off_bnd);
@@ -277,7 +283,7 @@ int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char 
         if (next_is_four(lv)) {
             TimingScope ts(LABSORT_K_MERGE4, s);
             HIP_TRY(launch_merge4_pass(cur, nxt, n, run, flip, bnd, samp[sb], next_is_four(lv + 2) ? samp[sb ^ 1] : nullptr,
-                                       s));
+                                       s, nullptr, nullptr, err));
             sb ^= 1;
             run *= 4;
             lv += 2;
@@ -501,10 +507,10 @@ int labsort_sort_device(const void *d_in, void *d_out, size_t n, int key_type, i
 
 namespace {
 // Synchronise the stream, then read the device error word (the workspace's first
-// word) when the sort that used the workspace had a radix layout.
-int read_status(const void *d_ws, bool radix_layout_used, hipStream_t s) {
+// word) when the sort that used the workspace had one (radix and merge layouts beyond one tile).
+int read_status(const void *d_ws, bool has_err_word, hipStream_t s) {
     HIP_TRY(hipStreamSynchronize(s));
-    if (!radix_layout_used) return LABSORT_OK;
+    if (!has_err_word) return LABSORT_OK;
     if (!d_ws) return LABSORT_ERR_ARG;
     uint32_t err = 0;
     HIP_TRY(hipMemcpyAsync(&err, d_ws, 4, hipMemcpyDeviceToHost, s));
@@ -516,12 +522,12 @@ int read_status(const void *d_ws, bool radix_layout_used, hipStream_t s) {
 int labsort_workspace_status(const void *d_ws, size_t n, int algo, void *stream) {
     if (n == 0) return read_status(d_ws, false, as_stream(stream));
     algo = resolve_algo(algo, n);
-    return read_status(d_ws, !small_path(n, algo) && algo != LABSORT_ALGO_MERGE, as_stream(stream));
+    return read_status(d_ws, !small_path(n, algo), as_stream(stream));
 }
 
 int labsort_pairs_workspace_status(const void *d_ws, size_t n, int algo, void *stream) {
     algo = resolve_pairs_algo(algo, n);
-    return read_status(d_ws, n > (size_t)TS_TILE_KV && algo == LABSORT_ALGO_RADIX, as_stream(stream));
+    return read_status(d_ws, n > (size_t)TS_TILE_KV, as_stream(stream));
 }
 
 namespace {
@@ -749,11 +755,13 @@ int pairs_merge_levels(size_t n) {
     return m;
 }
 struct PairsMergeLayout {
-    size_t off_tk, off_tv, off_bnd, off_samp[2], total;
+    size_t off_err, off_tk, off_tv, off_bnd, off_samp[2], total;
 };
 PairsMergeLayout pairs_merge_layout(size_t n) {
     PairsMergeLayout L{};
     size_t o = 0;
+    L.off_err = o;  // (first word: labsort_pairs_workspace_status)
+    o += 256;
     L.off_tk = o;
     o = align_up(o + n * 4, 256);
     L.off_tv = o;
@@ -855,6 +863,8 @@ int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void
     uint32_t *tk = reinterpret_cast<uint32_t *>(ws + L.off_tk), *tv = reinterpret_cast<uint32_t *>(ws + L.off_tv);
     uint32_t *bnd = reinterpret_cast<uint32_t *>(ws + L.off_bnd);
     uint32_t *samp[2] = {reinterpret_cast<uint32_t *>(ws + L.off_samp[0]), reinterpret_cast<uint32_t *>(ws + L.off_samp[1])};
+    uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
+    HIP_TRY(hipMemsetAsync(err, 0, 4, s));
     const int m = pairs_merge_levels(n);
     const bool four = LABSORT_MERGE4 && (((uintptr_t)ko | (uintptr_t)vo | (uintptr_t)tk | (uintptr_t)tv) & 15u) == 0;
     const int npass = four ? m / 2 + m % 2 : m;
@@ -871,7 +881,7 @@ int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void
         if (next_is_four(lv)) {
             TimingScope ts(LABSORT_K_MERGE4, s);
             HIP_TRY(launch_merge4_pass(ck, nk, n, run, flip, bnd, samp[sb], next_is_four(lv + 2) ? samp[sb ^ 1] : nullptr,
-                                       s, cv, nv));
+                                       s, cv, nv, err));
             sb ^= 1;
             run *= 4;
             lv += 2;

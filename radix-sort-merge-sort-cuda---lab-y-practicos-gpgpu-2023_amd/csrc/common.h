@@ -173,6 +173,7 @@ hipError_t launch_tile_sort_kv(const uint32_t *in, uint32_t *out, const uint32_t
 // four-way merge pass (merge4.hip): runs of r keys (a multiple of M4_S) -> runs of 4r;
 // bnd: merge4_bnd_words(n, r) words of workspace (16-B aligned); out 16-B aligned.
 // vin / vout (both or neither): 4-byte payloads carried with their keys (vout 16-B aligned).
+// err: set to 1 if a block's cuts are inconsistent (cannot happen; the block is skipped).
 // Samples: every M4_S-th key of a pass's output, samp[pos / M4_S] = out[pos] -- written by
 // the pass before a four-way pass (samp_out of the tile sort, the pairwise pass or a
 // four-way pass) and read by it (samp_in; nullptr: gathered by the pass itself).
@@ -181,7 +182,7 @@ inline size_t merge4_samp_words(size_t n) { return (n + M4_S - 1) / M4_S + 4; }
 size_t merge4_bnd_words(size_t n, size_t r);
 hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_t r, uint32_t flip, uint32_t *bnd,
                               const uint32_t *samp_in, uint32_t *samp_out, hipStream_t s, const uint32_t *vin = nullptr,
-                              uint32_t *vout = nullptr);
+                              uint32_t *vout = nullptr, uint32_t *err = nullptr);
 hipError_t launch_merge_ab(const uint32_t *a, size_t la, const uint32_t *b, size_t lb, uint32_t *out, size_t d0,
                            size_t d1, uint32_t flip, uint32_t *part, hipStream_t s);
 hipError_t launch_upper_bound(const uint32_t *keys, size_t n, uint32_t flip, const uint32_t *values, size_t nv,

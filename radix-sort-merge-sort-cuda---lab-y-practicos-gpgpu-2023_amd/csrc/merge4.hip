@@ -343,7 +343,8 @@ struct alignas(16) M4Smem {
 };
 
 struct M4Blk {
-    uint32_t g;  // group
+    uint32_t bad;  // inconsistent cuts (cannot happen): the block is skipped and reported
+    uint32_t g;    // group
     uint32_t lo[4], len[4];
     uint32_t out;  // output position of the block's first key
     uint32_t tot;
@@ -374,10 +375,13 @@ __device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *lo, uint3
     q.out = g * 4u * G.r + l4.x + l4.y + l4.z + l4.w;
     q.tot = q.len[0] + q.len[1] + q.len[2] + q.len[3];
     // (cannot happen with consistent cuts; a broken table must not send loads or stores out
-    // of the runs: the block is skipped and the sort's output check fails instead)
+    // of the runs: the block is skipped and the kernel sets the workspace's error word, which
+    // labsort_workspace_status reports as LABSORT_ERR_DEVICE)
+    q.bad = 0u;
     if (h4.x < l4.x || h4.y < l4.y || h4.z < l4.z || h4.w < l4.w || h4.x > rl[0] || h4.y > rl[1] || h4.z > rl[2] ||
         h4.w > rl[3] || q.tot > M4_CAP - 2 * M4_KPT) {
         q.tot = 0u;
+        q.bad = 1u;
 #pragma unroll
         for (int j = 0; j < 4; ++j) q.len[j] = 0u;
     }
@@ -391,7 +395,7 @@ __device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *lo, uint3
 template <bool FLIP>
 __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                           M4Geo G, const uint4 *__restrict__ bnd, uint32_t per,
-                                                          uint32_t *__restrict__ samp_out) {
+                                                          uint32_t *__restrict__ samp_out, uint32_t *__restrict__ err) {
     constexpr uint32_t PADV = FLIP ? 0x7FFFFFFFu : 0xFFFFFFFFu;  // +inf in key order
     __shared__ M4Smem sm;
     const uint32_t tid = threadIdx.x;
@@ -448,6 +452,7 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
     uint32_t p = 0u;
     for (uint32_t id = b0; id < b1; ++id) {
         uint32_t *X = sm.buf[p], *Y = sm.buf[p ^ 1u];
+        if (cur.bad && err && tid == 0u) err[0] = 1u;
         const uint32_t la = cur.len[0], lb = cur.len[1], lc = cur.len[2], ld = cur.len[3];
         const uint32_t oB = la + M4_PAD, oC = oB + lb + M4_PAD, oD = oC + lc + M4_PAD;  // LDS offsets (A at 0)
         const uint32_t lab = la + lb, lcd = lc + ld, nab = (lab + M4_KPT - 1) / M4_KPT, ncd = (lcd + M4_KPT - 1) / M4_KPT;
@@ -564,7 +569,7 @@ template <bool FLIP>
 __global__ __launch_bounds__(M4_BLOCK, 4) void k_m4_merge_kv(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                              const uint32_t *__restrict__ vsrc, uint32_t *__restrict__ vdst,
                                                              M4Geo G, const uint4 *__restrict__ bnd, uint32_t per,
-                                                             uint32_t *__restrict__ samp_out) {
+                                                             uint32_t *__restrict__ samp_out, uint32_t *__restrict__ err) {
     __shared__ M4SmemKV sm;
     const uint32_t tid = threadIdx.x;
     const uint32_t b0 = blockIdx.x * per;
@@ -616,6 +621,7 @@ __global__ __launch_bounds__(M4_BLOCK, 4) void k_m4_merge_kv(const uint32_t *__r
     uint32_t p = 0u;
     for (uint32_t id = b0; id < b1; ++id) {
         uint32_t *X = sm.buf[p], *Y = sm.buf[p ^ 1u], *XV = sm.vbuf[p], *YV = sm.vbuf[p ^ 1u];
+        if (cur.bad && err && tid == 0u) err[0] = 1u;
         const uint32_t la = cur.len[0], lb = cur.len[1], lc = cur.len[2], ld = cur.len[3];
         const uint32_t oB = la + M4_PAD, oC = oB + lb + M4_PAD, oD = oC + lc + M4_PAD;
         const uint32_t lab = la + lb, lcd = lc + ld, nab = (lab + M4_KPT - 1) / M4_KPT;
@@ -713,7 +719,7 @@ size_t merge4_bnd_words(size_t n, size_t r) {
 
 hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_t r, uint32_t flip, uint32_t *bnd,
                               const uint32_t *samp_in, uint32_t *samp_out, hipStream_t s, const uint32_t *vin,
-                              uint32_t *vout) {
+                              uint32_t *vout, uint32_t *err) {
     if (n == 0) return hipSuccess;
     if (r % M4_S || n > 0xFFFFFFFFull - 4 * r || !vin != !vout) return hipErrorInvalidValue;
     if ((((uintptr_t)out | (uintptr_t)vout) & 15u) != 0) return hipErrorInvalidValue;  // 16-B stores
@@ -741,15 +747,15 @@ hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_
         if (pkv > M4_MAX_PER) pkv = M4_MAX_PER;
         const uint32_t gkv = (G.nblocks + pkv - 1) / pkv;
         if (flip)
-            k_m4_merge_kv<true><<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, reinterpret_cast<const uint4 *>(bnd), pkv, samp_out);
+            k_m4_merge_kv<true><<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, reinterpret_cast<const uint4 *>(bnd), pkv, samp_out, err);
         else
-            k_m4_merge_kv<false><<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, reinterpret_cast<const uint4 *>(bnd), pkv, samp_out);
+            k_m4_merge_kv<false><<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, reinterpret_cast<const uint4 *>(bnd), pkv, samp_out, err);
         return hipGetLastError();
     }
     if (flip)
-        k_m4_merge<true><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out);
+        k_m4_merge<true><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out, err);
     else
-        k_m4_merge<false><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out);
+        k_m4_merge<false><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out, err);
     return hipGetLastError();
 }
 

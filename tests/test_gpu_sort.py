@@ -434,11 +434,13 @@ def test_sort_device_segment_boundaries(ls, oracle, torch_gpu, n):
     np.testing.assert_array_equal(from_dev(t), oracle.sort_u32(a))
 
 
+@pytest.mark.parametrize("algo", ["radix", "merge"])
 @pytest.mark.parametrize("pairs", [False, True])
-def test_workspace_status_reports_device_error(ls, oracle, torch_gpu, pairs):
-    """A radix sort that a kernel flagged (look-back spin limit) is reported as
-    LABSORT_ERR_DEVICE by labsort_workspace_status, never as OK; the next sort on the
-    workspace clears the word.  The error word is the workspace's first word."""
+def test_workspace_status_reports_device_error(ls, oracle, torch_gpu, pairs, algo):
+    """A sort that a kernel flagged (radix: the look-back spin limit; merge: a four-way
+    block with inconsistent cuts, skipped) is reported as LABSORT_ERR_DEVICE by
+    labsort_workspace_status, never as OK; the next sort on the workspace clears the word.
+    The error word is the workspace's first word in both layouts."""
     torch = torch_gpu
     n = 1 << 20
     t = torch.empty(n, dtype=torch.int32, device="cuda")
@@ -446,20 +448,18 @@ def test_workspace_status_reports_device_error(ls, oracle, torch_gpu, pairs):
     o = torch.empty_like(t)
     if pairs:
         v, vo = torch.arange(n, dtype=torch.int32, device="cuda"), torch.empty_like(t)
-        ws = torch.empty(ls.pairs_workspace_bytes(n, "radix"), dtype=torch.uint8, device="cuda")
-        run = lambda: ls.sort_pairs_device(t, v, o, vo, n, algo="radix", workspace=ws)  # noqa: E731
-        status = lambda: ls.pairs_workspace_status(ws, n, "radix")  # noqa: E731
+        ws = torch.empty(ls.pairs_workspace_bytes(n, algo), dtype=torch.uint8, device="cuda")
+        run = lambda: ls.sort_pairs_device(t, v, o, vo, n, algo=algo, workspace=ws)  # noqa: E731
+        status = lambda: ls.pairs_workspace_status(ws, n, algo)  # noqa: E731
     else:
-        ws = torch.empty(ls.workspace_bytes(n, "radix"), dtype=torch.uint8, device="cuda")
-        run = lambda: ls.sort_device(t, o, n, algo="radix", workspace=ws)  # noqa: E731
-        status = lambda: ls.workspace_status(ws, n, "radix")  # noqa: E731
+        ws = torch.empty(ls.workspace_bytes(n, algo), dtype=torch.uint8, device="cuda")
+        run = lambda: ls.sort_device(t, o, n, algo=algo, workspace=ws)  # noqa: E731
+        status = lambda: ls.workspace_status(ws, n, algo)  # noqa: E731
     run()
     status()  # clean sort: OK
-    ws[:4].view(torch.int32).fill_(1)  # what atomicOr(err, 1) leaves behind
+    ws[:4].view(torch.int32).fill_(1)  # what the kernels' error store leaves behind
     with pytest.raises(ls.LabsortError, match="device-side"):
         status()
-    # merge-path sorts have no error word: always OK
-    ls.workspace_status(ws, n, "merge")
     run()
     status()
     np.testing.assert_array_equal(from_dev(o), oracle.sort_u32(oracle.gen(n, SEED + 40, "u32")))
