@@ -9,9 +9,9 @@
 // (merge_segments_kernel :272-300).  Here, over four runs A, B, C, D of a group:
 //   k_m4_rank  every M4_S-th key of every run is a sample; a sample's index in the merged
 //              order of all the group's samples, under the order (key, run, position), is
-//              its own index plus, per other run, the samples that precede it (binary
-//              search over that run's samples: upper bound for earlier runs, lower bound
-//              for later ones -- the reference's tie rule generalised to four runs).  Every
+//              its own index plus, per other run, the samples that precede it (searched
+//              over that run's samples: upper bound for earlier runs, lower bound for
+//              later ones -- the reference's tie rule generalised to four runs).  Every
 //              M4_M-th sample in that order is a block boundary: its co-rank in each other
 //              run (the same bound over the run's keys, bracketed to one sample gap) gives
 //              the boundary's four cuts.  A block between consecutive boundaries holds at
@@ -24,7 +24,11 @@
 //              bitonic network in registers (equal keys are identical words, so the order
 //              among them does not change the output): A+B and C+D into LDS, then
 //              (A+B)+(C+D) into an LDS staging buffer aligned to the block's output offset,
-//              stored as 16-B nontemporal stores.
+//              stored as 16-B nontemporal stores (and every M4_S-th output word as the next
+//              four-way pass's sample).
+//   k_m4_merge_kv the same with 4-byte payloads beside the keys, stable level merges.
+// r29 at 2^28 (profiles/r29_ab_merge4_v2.txt): merge sort 6.79 -> 6.04 ms
+// (pass 0.745 ms: rank 0.077 + merge 0.68, VALU- and LDS-bound), key/value 13.95 -> 11.61 ms.
 #include "common.h"
 #include "devutil.h"
 
