@@ -532,11 +532,10 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
 
 // Key/value four-way merge (payloads of 4 bytes; labsort_sort_pairs_device with
 // LABSORT_ALGO_MERGE).  The same blocks, rank and schedule as k_m4_merge, with every key's
-// payload carried beside it through both LDS buffers; each level is the stable merge of the
-// pairwise key/value pass (co-rank, then the thread's 8 outputs taken in turn, "A before
-// equal B" -- lab.cu:163-170 -- each output remembering the LDS slot it came from, the
-// payloads read from those slots afterwards).  The four-way order (key, run, position) and
-// the runs' input order make the merge sort stable, as the pairwise passes were.
+// payload carried beside it through both LDS buffers; each level merges stably ("A before
+// equal B", lab.cu:163-170) by sorting (key, slot) words, m4_merge8_kv.  The four-way
+// order (key, run, position) and the runs' input order make the merge sort stable, as the
+// pairwise passes were.
 struct alignas(16) M4SmemKV {
     alignas(16) uint32_t buf[2][M4_BUFW];
     alignas(16) uint32_t vbuf[2][M4_BUFW];
@@ -544,29 +543,41 @@ struct alignas(16) M4SmemKV {
 };
 
 // the thread's 8 outputs at diagonal d of the stable merge of K[oa, oa + la) and
-// K[ob, ob + lb) (keys r, payloads pv from V at the same slots)
+// K[ob, ob + lb): the bitonic network of the keys-only pass on (key, LDS slot) words -- A's
+// slots precede B's, so equal keys keep "A before B" and each run's own order -- and the
+// payloads read from the winners' slots (r29: 1.366 vs 1.410 ms per pass against the
+// pairwise pass's sequential stable merge, 8 dependent LDS reads per thread and level)
 template <bool FLIP>
 __device__ __forceinline__ void m4_merge8_kv(const uint32_t *K, const uint32_t *V, uint32_t oa, uint32_t la, uint32_t ob,
                                              uint32_t lb, uint32_t d, uint32_t (&r)[M4_KPT], uint32_t (&pv)[M4_KPT]) {
     constexpr uint32_t flip = FLIP ? 0x80000000u : 0u;
-    uint32_t ai = m4_corank<FLIP>(K + oa, la, K + ob, lb, d), bi = d - ai;
-    uint32_t va = ai < la ? K[oa + ai] : 0u, vb = bi < lb ? K[ob + bi] : 0u;
-    uint32_t from[M4_KPT];
+    const uint32_t ai = m4_corank<FLIP>(K + oa, la, K + ob, lb, d), bi = d - ai;
+    uint64_t x[2 * M4_KPT];
 #pragma unroll
     for (int j = 0; j < M4_KPT; ++j) {
-        const bool takeA = bi >= lb || (ai < la && (va ^ flip) <= (vb ^ flip));
-        r[j] = takeA ? va : vb;
-        from[j] = takeA ? oa + ai : ob + bi;
-        if (takeA) {
-            ++ai;
-            va = ai < la ? K[oa + ai] : 0u;
-        } else {
-            ++bi;
-            vb = bi < lb ? K[ob + bi] : 0u;
+        const uint32_t ia = ai + (uint32_t)j, ib = bi + (uint32_t)j;
+        const uint32_t ka = K[oa + (ia < la ? ia : 0u)] ^ flip, kb = K[ob + (ib < lb ? ib : 0u)] ^ flip;
+        x[j] = ia < la ? ((uint64_t)ka << 32 | (oa + ia)) : ~0ull;
+        x[2 * M4_KPT - 1 - j] = ib < lb ? ((uint64_t)kb << 32 | (ob + ib)) : ~0ull;
+    }
+#pragma unroll
+    for (int st = M4_KPT; st >= 1; st >>= 1) {
+#pragma unroll
+        for (int i = 0; i < 2 * M4_KPT; ++i) {
+            if ((i & st) == 0) {
+                const uint64_t lo = x[i] < x[i + st] ? x[i] : x[i + st], hi = x[i] < x[i + st] ? x[i + st] : x[i];
+                x[i] = lo;
+                x[i + st] = hi;
+            }
         }
     }
 #pragma unroll
-    for (int j = 0; j < M4_KPT; ++j) pv[j] = V[from[j]];
+    for (int j = 0; j < M4_KPT; ++j) r[j] = (uint32_t)(x[j] >> 32) ^ flip;
+#pragma unroll
+    for (int j = 0; j < M4_KPT; ++j) {
+        const uint32_t sl = (uint32_t)x[j];  // (past both windows: an unused output, any valid slot)
+        pv[j] = V[sl < M4_BUFW ? sl : 0u];
+    }
 }
 
 template <bool FLIP>
