@@ -396,7 +396,9 @@ __device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *lo, uint3
 // a block takes three barriers: keys in X -> level 1 into Y -> level 2 back into X (staging)
 // -> the stores read X while the next block's keys go into Y, which becomes its X (r29: four
 // barriers with fixed in / mid / staging roles, 0.685 ms per pass at 2^28)
-template <bool FLIP>
+// WIDE: groups of more than 2^30 keys (runs of 2^29, n > 2^30): 64-bit byte offsets from
+// the group base (below that a 32-bit offset, added to the base in the load's address)
+template <bool FLIP, bool WIDE>
 __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                           M4Geo G, const uint4 *__restrict__ bnd, uint32_t per,
                                                           uint32_t *__restrict__ samp_out, uint32_t *__restrict__ err) {
@@ -420,7 +422,8 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
             dd = i >= o1 ? d1 : dd;
             dd = i >= o2 ? d2 : dd;
             dd = i >= o3 ? d3 : dd;
-            v[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(gb + (uint32_t)((i + dd) * 4u))) : PADV;
+            const size_t off = WIDE ? (size_t)(i + dd) * 4u : (size_t)(uint32_t)((i + dd) * 4u);
+            v[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(gb + off)) : PADV;
         }
     };
     // block q's keys (registers v) into X with a pad of +inf after each window
@@ -580,7 +583,7 @@ __device__ __forceinline__ void m4_merge8_kv(const uint32_t *K, const uint32_t *
     }
 }
 
-template <bool FLIP>
+template <bool FLIP, bool WIDE>
 __global__ __launch_bounds__(M4_BLOCK, 4) void k_m4_merge_kv(const uint32_t *__restrict__ src, uint32_t *__restrict__ dst,
                                                              const uint32_t *__restrict__ vsrc, uint32_t *__restrict__ vdst,
                                                              M4Geo G, const uint4 *__restrict__ bnd, uint32_t per,
@@ -604,7 +607,7 @@ __global__ __launch_bounds__(M4_BLOCK, 4) void k_m4_merge_kv(const uint32_t *__r
             dd = i >= o1 ? d1 : dd;
             dd = i >= o2 ? d2 : dd;
             dd = i >= o3 ? d3 : dd;
-            const uint32_t off = (i + dd) * 4u;
+            const size_t off = WIDE ? (size_t)(i + dd) * 4u : (size_t)(uint32_t)((i + dd) * 4u);
             v[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(gb + off)) : 0u;
             pl[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(vb + off)) : 0u;
         }
@@ -756,21 +759,21 @@ hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_
     uint32_t per = (G.nblocks + want - 1) / want;
     if (per > M4_MAX_PER) per = M4_MAX_PER;
     const uint32_t g = (G.nblocks + per - 1) / per;
+    const bool wide = r > ((size_t)1 << 28);  // a group's byte offsets pass 2^32
+    const uint4 *bt = reinterpret_cast<const uint4 *>(bnd);
     if (vin) {
         const uint32_t want_kv = (uint32_t)(2 * (cus > 0 ? cus : 256));  // two 70 KB workgroups per CU
         uint32_t pkv = (G.nblocks + want_kv - 1) / want_kv;
         if (pkv > M4_MAX_PER) pkv = M4_MAX_PER;
         const uint32_t gkv = (G.nblocks + pkv - 1) / pkv;
-        if (flip)
-            k_m4_merge_kv<true><<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, reinterpret_cast<const uint4 *>(bnd), pkv, samp_out, err);
-        else
-            k_m4_merge_kv<false><<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, reinterpret_cast<const uint4 *>(bnd), pkv, samp_out, err);
+        auto kv = flip ? (wide ? k_m4_merge_kv<true, true> : k_m4_merge_kv<true, false>)
+                       : (wide ? k_m4_merge_kv<false, true> : k_m4_merge_kv<false, false>);
+        kv<<<gkv, M4_BLOCK, 0, s>>>(in, out, vin, vout, G, bt, pkv, samp_out, err);
         return hipGetLastError();
     }
-    if (flip)
-        k_m4_merge<true><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out, err);
-    else
-        k_m4_merge<false><<<g, M4_BLOCK, 0, s>>>(in, out, G, reinterpret_cast<const uint4 *>(bnd), per, samp_out, err);
+    auto k = flip ? (wide ? k_m4_merge<true, true> : k_m4_merge<true, false>)
+                  : (wide ? k_m4_merge<false, true> : k_m4_merge<false, false>);
+    k<<<g, M4_BLOCK, 0, s>>>(in, out, G, bt, per, samp_out, err);
     return hipGetLastError();
 }
 

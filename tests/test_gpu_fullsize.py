@@ -71,6 +71,40 @@ def test_fullsize_2e30_merge(ls, torch_gpu):
     assert sha(got) == c["sha256_sorted_u32"]
 
 
+@pytest.mark.parametrize("key,n", [("u32", (1 << 30) + 4097), ("i32", (1 << 30) + 4097), ("u32", (1 << 31) - 1)])
+def test_fullsize_past_2e30_merge(ls, torch_gpu, key, n):
+    """2^30 + 4097 keys and the merge path's maximum, 2^31 - 1: the last four-way pass
+    merges runs of 2^29 (a group of up to 2^31 keys, byte offsets past 2^32 from its base;
+    32-bit offsets read wrapped keys there before r29's fix). No fixture covers these
+    size and a CPU sort of it takes minutes, so the result is checked by size-independent
+    properties: no descent (labsort_count_descents), and the same multiset as the input
+    (the four 8-bit digit histograms, the sum and the sum of squares mod 2^64)."""
+    torch = torch_gpu
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, 0x5EED0031, "u32")
+    o = torch.empty_like(t)
+    ls.sort_device(t, o, n, key=key, algo="merge")
+    torch.cuda.synchronize()
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ls.count_descents(o, n, cnt, key=key)
+    hs = torch.zeros(4 * 256, dtype=torch.int32, device="cuda")
+    ho = torch.zeros(4 * 256, dtype=torch.int32, device="cuda")
+    ls.histogram(t, n, hs, bits=8, key=key)
+    ls.histogram(o, n, ho, bits=8, key=key)
+
+    def fp(x):
+        s1 = s2 = 0
+        for part in torch.split(x, 1 << 27):
+            v = part.to(torch.int64) & 0xFFFFFFFF
+            s1 += int(v.sum().item())
+            s2 = (s2 + int((v * v).sum().item())) & (2**64 - 1)
+        return s1, s2
+
+    assert int(cnt.item()) == 0
+    assert torch.equal(hs, ho)
+    assert fp(t) == fp(o)
+
+
 def test_fullsize_inplace_repeat(ls, torch_gpu):
     """Same 2^28 input sorted 3 times in place and out of place: identical results
     (the look-back protocol is deterministic whatever the tile timing)."""
