@@ -105,6 +105,34 @@ def test_fullsize_past_2e30_merge(ls, torch_gpu, key, n):
     assert fp(t) == fp(o)
 
 
+def test_fullsize_past_2e30_merge_pairs(ls, torch_gpu):
+    """Key/value merge sort of 2^30 + 4097 (key, index) pairs: the key/value four-way
+    pass's 64-bit offsets.  Checked chunk by chunk: keys without descent, every payload's
+    input key equal to its output key, equal keys in input order (stable), payloads a
+    permutation (their sum)."""
+    torch = torch_gpu
+    n = (1 << 30) + 4097
+    k = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(k, n, 0x5EED0032, "lowbits", param=20)  # 2^20 distinct keys: ~1000 copies each
+    v = torch.arange(n, dtype=torch.int32, device="cuda")
+    ko, vo = torch.empty_like(k), torch.empty_like(v)
+    ls.sort_pairs_device(k, v, ko, vo, n, key="u32", algo="merge")
+    torch.cuda.synchronize()
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ls.count_descents(ko, n, cnt, key="u32")
+    assert int(cnt.item()) == 0
+    total = 0
+    step = 1 << 27
+    for a in range(0, n, step):
+        b = min(n, a + step + 1)  # one past the chunk: the pair across the chunk edge
+        idx = vo[a:b].to(torch.int64)
+        assert torch.equal(k[idx], ko[a:b])
+        same = ko[a + 1:b] == ko[a:b - 1]
+        assert bool((vo[a + 1:b][same] > vo[a:b - 1][same]).all())
+        total += int(idx[: min(step, n - a)].sum().item())
+    assert total == n * (n - 1) // 2
+
+
 def test_fullsize_inplace_repeat(ls, torch_gpu):
     """Same 2^28 input sorted 3 times in place and out of place: identical results
     (the look-back protocol is deterministic whatever the tile timing)."""
