@@ -261,7 +261,7 @@ int sort_radix(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, int b
 int sort_merge(const uint32_t *in, uint32_t *out, size_t n, uint32_t flip, char *ws, hipStream_t s) {
     const MergeLayout L = merge_layout(n);
     uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
-    HIP_TRY(hipMemsetAsync(err, 0, 4, s));
+    HIP_TRY(launch_zero(err, 16, s));  // (a kernel: graph-replayable)
     uint32_t *tmp = reinterpret_cast<uint32_t *>(ws + L.off_tmp);
     uint32_t *part = reinterpret_cast<uint32_t *>(ws + L.off_part);
     uint32_t *bnd = reinterpret_cast<uint32_t *>(ws + L.off_bnd);
@@ -592,7 +592,7 @@ int sort_host_pipelined(DeviceCache &c, void *h_keys, size_t n, int key_type, in
             HIP_TRY(hipEventRecord(c.ev[i], c.copy));
             HIP_TRY(hipStreamWaitEvent(c.stream, c.ev[i], 0));
             if ((st = labsort_sort_device(X + o, Y + o, len, key_type, calgo, c.ws, c.ws_bytes, c.stream))) return st;
-            if (!small_path(len, calgo) && calgo != LABSORT_ALGO_MERGE)  // the radix layout's error word
+            if (!small_path(len, calgo))  // the workspace's error word (radix and merge layouts)
                 HIP_TRY(hipMemcpyAsync(errs + i, c.ws, 4, hipMemcpyDeviceToDevice, c.stream));
         }
         if (i == HOST_CHUNKS / 2 - 1 && (st = merge_half(0))) return st;
@@ -864,7 +864,7 @@ int labsort_sort_pairs_device(const void *d_keys_in, const void *d_vals_in, void
     uint32_t *bnd = reinterpret_cast<uint32_t *>(ws + L.off_bnd);
     uint32_t *samp[2] = {reinterpret_cast<uint32_t *>(ws + L.off_samp[0]), reinterpret_cast<uint32_t *>(ws + L.off_samp[1])};
     uint32_t *err = reinterpret_cast<uint32_t *>(ws + L.off_err);
-    HIP_TRY(hipMemsetAsync(err, 0, 4, s));
+    HIP_TRY(launch_zero(err, 16, s));  // (a kernel: graph-replayable)
     const int m = pairs_merge_levels(n);
     const bool four = LABSORT_MERGE4 && (((uintptr_t)ko | (uintptr_t)vo | (uintptr_t)tk | (uintptr_t)tv) & 15u) == 0;
     const int npass = four ? m / 2 + m % 2 : m;
