@@ -10,17 +10,22 @@
 //                     tile per wave, 1-bit split per iteration with ballot/mbcnt
 //                     (the split's scan) and ds_permute (the scatter), early exit
 //                     when the tile is sorted (:61).
-//   k_histogram       letra.pdf's global "totalFalses" generalised to 8-bit digits,
-//                     all passes in one read of the keys.
-//   k_onesweep        one LSD pass: block-local rank (wave64 match + per-wave
-//                     counters), decoupled look-back for the global exclusive
-//                     offsets, LDS reorder, coalesced scatter.
+//   k_hist_seg        letra.pdf's global "totalFalses" generalised to 8-bit digits:
+//                     digit 0 per position segment and the joint fields that size the
+//                     later passes' segments, in one read of the keys (k_histogram:
+//                     the plain form); k_plan8 turns them into every pass's plan.
+//   k_onesweep_p      one persistent LSD pass (the default radix above 2^25 keys): lane-
+//                     ordered LDS-atomic rank, segmented decoupled look-back for the
+//                     global offsets, LDS reorder, coalesced scatter; <true>: key/value.
+//                     (k_onesweep: the non-persistent form, 1-bit digits for radix1.)
 //   k_tile_sort       stage 1+2 of order_array (lab.cu:323-346): an LDS-resident
-//                     8192-key LSD radix sort per workgroup.
-//   k_merge_*         stage 3 (separators_kernel :209-270 + merge_segments_kernel
-//                     :272-300) as merge-path: a co-rank search per output tile
-//                     (busquedaPorBiparticion :102-132, same tie rule: A before B
-//                     on equal keys) and an LDS merge per tile.
+//                     32768-key (16384 pairs) LSD radix sort per workgroup.
+//   k_merge_pass_p    stage 3 (separators_kernel :209-270 + merge_segments_kernel
+//                     :272-300) as merge-path: co-rank searches per output tile
+//                     (busquedaPorBiparticion :102-132, same tie rule: A before B on
+//                     equal keys) and an LDS merge per tile; k_merge_ab: two arrays.
+//                     The four-way pass of the merge sort is in merge4.hip, the
+//                     gathered radix (2^16 <= n < 2^25) in gsweep.hip.
 #include "common.h"
 #include "devutil.h"
 
