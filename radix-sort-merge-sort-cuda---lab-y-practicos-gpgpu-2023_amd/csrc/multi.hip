@@ -1099,8 +1099,10 @@ int labsort_comm_destroy(labsort_comm_t c) {
     if (!c) return LABSORT_OK;
     int st = LABSORT_OK;
     if (c->rc.nc) {
+        // (a nonblocking communicator may report its teardown as still in progress: not
+        // an error, its resources are released when it completes)
         const ncclResult_t r = g_rccl.destroy(c->rc.nc);
-        if (r != ncclSuccess) st = g_rccl.fail("ncclCommDestroy", r);
+        if (r != ncclSuccess && r != ncclInProgress) st = g_rccl.fail("ncclCommDestroy", r);
     }
     if (c->R.dev >= 0) {
         (void)hipSetDevice(c->R.dev);
