@@ -514,7 +514,10 @@ def dist_main(args, torch, ls, world, rank, dev):
         sys.exit(3)
     dist.barrier()
     if dcomm is not None:
-        dcomm.close()
+        try:  # (a teardown error is reported, not allowed to lose the measured line)
+            dcomm.close()
+        except Exception as e:  # noqa: BLE001
+            print(f"bench.py: rank {rank}: communicator teardown: {e}", file=sys.stderr)
     dist.destroy_process_group()
     # the host-pointer leg runs once every rank is done with its GPU
     hostp = host_leg(args) if rank == 0 and not args.no_host_path and args.backend == "nccl" else None
