@@ -91,13 +91,44 @@ constexpr uint32_t M4_RSPT = 2;                // samples per thread
 constexpr uint32_t M4_RT = M4_RB * M4_RSPT;    // samples per rank workgroup
 constexpr uint32_t M4_RW = 1024;               // most samples of another run held in LDS per workgroup
 
+// one round of the cut search: A - 1 probes of each of the three runs loaded at once, each
+// run's range [lo, hi] narrowed A-fold
+template <int A>
+__device__ __forceinline__ void m4_cut_round(const uint32_t *const (&run)[3], uint32_t (&lo)[3], uint32_t (&hi)[3],
+                                             const bool (&le)[3], uint32_t xf, uint32_t flip) {
+    uint32_t v[3][A - 1], step[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        step[i] = (hi[i] - lo[i] + (uint32_t)(A - 1)) / (uint32_t)A;
+#pragma unroll
+        for (int p = 0; p < A - 1; ++p) {  // probe key lo + (p + 1) step - 1, clamped into the run (unused then)
+            const uint32_t idx = lo[i] + (uint32_t)(p + 1) * step[i] - 1u;
+            const uint32_t top = hi[i] ? hi[i] - 1u : 0u;
+            v[i][p] = run[i][idx < top ? idx : top];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        uint32_t t = 0u;
+#pragma unroll
+        for (int p = 0; p < A - 1; ++p) {
+            const uint32_t idx = lo[i] + (uint32_t)(p + 1) * step[i] - 1u, vf = v[i][p] ^ flip;
+            t += (idx < hi[i] && (vf < xf || (le[i] && vf == xf))) ? 1u : 0u;
+        }
+        const uint32_t nhi = lo[i] + (t + 1u) * step[i] - 1u;  // probe t failed (none does when t = A - 1)
+        hi[i] = step[i] && t < (uint32_t)(A - 1) ? (nhi < hi[i] ? nhi : hi[i]) : hi[i];
+        lo[i] += t * step[i];
+    }
+}
+
 // a boundary sample (merged index m, a multiple of M4_M): its cut in every run -- in run j
 // between the last preceding sample and the next, so within one sample gap.  The other three
 // runs are searched together, 8-ary: each round loads 7 probes of every run at once and
 // narrows each gap 8-fold, so the < M4_S keys of a gap take 3 rounds of loads.  (r29, per pass
 // at 2^28: one binary search per run in turn, 21 dependent HBM loads, left the rank kernel at
 // 0.075 ms, 0.047 without any cut; 16 + 7 probes per run written with conditional loads,
-// which the compiler serialised, 0.149 ms.)
+// which the compiler serialised, 0.149 ms; r30: 15 + 7 probes in two rounds of m4_cut_round,
+// 0.090 against 0.075 ms for the three rounds.)
 __device__ __forceinline__ void m4_write_cut(const uint32_t *src, const M4Geo &G, uint32_t flip, uint32_t g, uint32_t k,
                                              uint32_t q, uint32_t x, const uint32_t (&cnt)[4], const uint32_t (&len)[4],
                                              uint4 *bnd) {
@@ -119,31 +150,7 @@ __device__ __forceinline__ void m4_write_cut(const uint32_t *src, const M4Geo &G
         hi[i] = hi[i] < lo[i] ? lo[i] : hi[i];
     }
 #pragma unroll
-    for (int round = 0; round < 3; ++round) {
-        uint32_t v[3][7], step[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            step[i] = (hi[i] - lo[i] + 7u) / 8u;
-#pragma unroll
-            for (int p = 0; p < 7; ++p) {  // probe key lo + (p + 1) step - 1, clamped into the run (unused then)
-                const uint32_t idx = lo[i] + (uint32_t)(p + 1) * step[i] - 1u;
-                const uint32_t top = hi[i] ? hi[i] - 1u : 0u;
-                v[i][p] = run[i][idx < top ? idx : top];
-            }
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            uint32_t t = 0u;
-#pragma unroll
-            for (int p = 0; p < 7; ++p) {
-                const uint32_t idx = lo[i] + (uint32_t)(p + 1) * step[i] - 1u, vf = v[i][p] ^ flip;
-                t += (idx < hi[i] && (vf < xf || (le[i] && vf == xf))) ? 1u : 0u;
-            }
-            const uint32_t nhi = lo[i] + (t + 1u) * step[i] - 1u;  // probe t failed (none does when t = 7)
-            hi[i] = step[i] && t < 7u ? (nhi < hi[i] ? nhi : hi[i]) : hi[i];
-            lo[i] += t * step[i];
-        }
-    }
+    for (int round = 0; round < 3; ++round) m4_cut_round<8>(run, lo, hi, le, xf, flip);
     uint32_t cut[4];
 #pragma unroll
     for (int i = 0; i < 3; ++i) cut[i + (i >= (int)k)] = lo[i];
@@ -256,15 +263,34 @@ __global__ __launch_bounds__(M4_RB) void k_m4_rank(const uint32_t *__restrict__ 
             }
         }
     }
+    // the thread's boundary samples (about one in M4_M) taken one per round: a wave runs the
+    // cut's three dependent load rounds once when no lane holds two boundaries, instead of
+    // once per sample slot (r30 at 2^28: 0.077 -> 0.070 ms and 0.087 -> 0.075 ms per pass on
+    // two boxes; two rounds, 16-ary then 8-ary, 0.090 ms: profiles/r30_ab_rank_cuts.txt)
+    uint32_t pend = 0u;
 #pragma unroll
     for (uint32_t e = 0; e < M4_RSPT; ++e) {
         const uint32_t q = q0 + tid + e * M4_RB;
-        if (q >= ns[k]) continue;
-        uint32_t cnt[4];
-        cnt[k] = 0u;
+        const uint32_t m = q + c[e][0] + c[e][1] + c[e][2];
+        if (q < ns[k] && m != 0u && m % M4_M == 0u) pend |= 1u << e;
+    }
+    while (__any(pend != 0u)) {
+        if (pend != 0u) {
+            const uint32_t e = (uint32_t)__builtin_ctz(pend);
+            pend &= pend - 1u;
+            uint32_t cnt[4], cc[3], x = 0u;
 #pragma unroll
-        for (int i = 0; i < 3; ++i) cnt[i + (i >= (int)k)] = c[e][i];
-        m4_write_cut(src, G, flip, g, k, q, xf[e] ^ flip, cnt, len, bnd);
+            for (uint32_t ee = 0; ee < M4_RSPT; ++ee)
+                if (ee == e) {
+                    x = xf[ee];
+#pragma unroll
+                    for (int i = 0; i < 3; ++i) cc[i] = c[ee][i];
+                }
+            cnt[k] = 0u;
+#pragma unroll
+            for (int i = 0; i < 3; ++i) cnt[i + (i >= (int)k)] = cc[i];
+            m4_write_cut(src, G, flip, g, k, q0 + tid + e * M4_RB, x ^ flip, cnt, len, bnd);
+        }
     }
 }
 
