@@ -177,7 +177,10 @@ hipError_t launch_tile_sort_kv(const uint32_t *in, uint32_t *out, const uint32_t
 // Samples: every M4_S-th key of a pass's output, samp[pos / M4_S] = out[pos] -- written by
 // the pass before a four-way pass (samp_out of the tile sort, the pairwise pass or a
 // four-way pass) and read by it (samp_in; nullptr: gathered by the pass itself).
-constexpr uint32_t M4_S = 128;
+#ifndef LABSORT_M4_S
+#define LABSORT_M4_S 128
+#endif
+constexpr uint32_t M4_S = LABSORT_M4_S;
 inline size_t merge4_samp_words(size_t n) { return (n + M4_S - 1) / M4_S + 4; }
 size_t merge4_bnd_words(size_t n, size_t r);
 hipError_t launch_merge4_pass(const uint32_t *in, uint32_t *out, size_t n, size_t r, uint32_t flip, uint32_t *bnd,

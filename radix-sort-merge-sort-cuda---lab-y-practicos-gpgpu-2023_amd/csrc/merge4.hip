@@ -35,7 +35,12 @@
 namespace labsort {
 
 // M4_S (common.h): sample stride (keys)
-constexpr uint32_t M4_M = 28;    // samples per block (merged order)
+// (M4_S 128 / M4_M 28 measured against 64 / 60, 64 / 56 and 256 / 12 in r30: 6.08 ms per
+// 2^28 merge sort against 6.37, 6.42 and 6.39; profiles/r30_ab_sample_stride.txt)
+#ifndef LABSORT_M4_M
+#define LABSORT_M4_M 28
+#endif
+constexpr uint32_t M4_M = LABSORT_M4_M;  // samples per block (merged order)
 constexpr int M4_KPT = 8;                // outputs per thread and merge level (r29: 16, with 256
 constexpr int M4_BLOCK = 4096 / M4_KPT;  // threads and half the co-rank searches, measured equal)
 constexpr uint32_t M4_CAP = (uint32_t)(M4_BLOCK * M4_KPT);  // keys per block at most
