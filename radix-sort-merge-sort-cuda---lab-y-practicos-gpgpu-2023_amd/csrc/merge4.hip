@@ -172,7 +172,14 @@ __device__ __forceinline__ void m4_write_cut(const uint32_t *src, const M4Geo &G
 // LDS.  r29 at 2^28, per pass: one full binary search per sample and run 0.116 ms (a chain
 // of log2(r / M4_S) scattered L2 loads); this form 0.074-0.078 ms with 1 or 2 samples per
 // thread, 0.101 with 4.
-__global__ __launch_bounds__(M4_RB) void k_m4_rank(const uint32_t *__restrict__ src, M4Geo G, uint32_t flip,
+// waves per SIMD the register budget is set for: 6 = 80 VGPRs, 19 of them spilled (r30:
+// 0.075 -> 0.072 ms per pass; 84 VGPRs, 5 waves, no spill before; 8 waves = 64 VGPRs, 62
+// spilled, 0.096 ms; profiles/r30_ab_rank_cuts.txt)
+#ifndef LABSORT_RANK_OCC
+#define LABSORT_RANK_OCC 6
+#endif
+#define M4_RANK_LB __launch_bounds__(M4_RB, LABSORT_RANK_OCC)
+__global__ M4_RANK_LB void k_m4_rank(const uint32_t *__restrict__ src, M4Geo G, uint32_t flip,
                                                    const uint32_t *__restrict__ samp, uint4 *__restrict__ bnd) {
     __shared__ uint32_t win[3][M4_RW];
     __shared__ uint32_t s_br[6];
