@@ -9,7 +9,9 @@ copies, lab.cu:321-397).  Keys are generated on the device (counter-based
 generator, seed 0x5EED0003) and stay resident in HBM; the sort is out of place
 so every step sorts the same input.
 
-N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): BASELINE config 5,
+N > 1 (one process per GPU, RCCL; started by torch.distributed.run, or -- when bench.py is
+invoked plainly with --gpus N -- by bench.py itself, which then launches the N ranks as one
+torch.distributed.run child tree with a deadline and relays rank 0's line): BASELINE config 5,
 the merge-sort path of the north_star through the product's C-ABI: a 2^30-key array
 (--total-log2n) partitioned over the N ranks (2^30/N keys each: strong scaling); every
 rank calls labsort_dist_sort on its communicator (labsort_comm_init_rccl, rank 0's unique
@@ -77,6 +79,8 @@ def parse():
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-pointer (PCIe-inclusive) leg")
     ap.add_argument("--host-log2n", type=int, default=30, help="host-pointer leg: keys = 2^host-log2n")
     ap.add_argument("--host-leg", default="", help=argparse.SUPPRESS)  # child of host_path: "peer" or "rccl"
+    ap.add_argument("--launch-timeout", type=float, default=900.0,
+                    help="N>1 started without torch.distributed.run: deadline for the N child ranks (s)")
     return ap.parse_args()
 
 
@@ -551,18 +555,92 @@ def dist_main(args, torch, ls, world, rank, dev):
     print(json.dumps(line), flush=True)
 
 
+def launch_ranks(args, torch) -> int:
+    """`python bench.py --gpus N` (N > 1) without torch.distributed.run around it: start the
+    N ranks here, as ONE child process tree (torch.distributed.run, 127.0.0.1 rendezvous)
+    before this process touches the GPU (torch.cuda.device_count() does not initialise it),
+    relay their output, and return non-zero unless rank 0 printed its config-5 line.  A
+    deadline (--launch-timeout) ends the whole tree (SIGTERM, then SIGKILL); torch.distributed.run
+    itself ends every rank when one fails.  With --backend nccl every rank needs its own GPU:
+    fewer visible devices than N is refused at once."""
+    import signal
+    import socket
+    import subprocess
+    import threading
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and ndev < args.gpus:
+        print(f"bench.py: --gpus {args.gpus} with --backend nccl needs {args.gpus} GPUs, {ndev} visible "
+              "(one rank per GPU); --backend gloo rehearses several ranks on one GPU", file=sys.stderr)
+        return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    drop = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+            "ROLE_RANK", "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")
+    env = {k: v for k, v in os.environ.items() if k not in drop}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env["PYTHONUNBUFFERED"] = "1"
+    cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    expired = threading.Event()
+
+    def deadline():
+        expired.set()
+        for sig, wait in ((signal.SIGTERM, 10), (signal.SIGKILL, 0)):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                return
+            try:
+                p.wait(timeout=wait) if wait else None
+                return
+            except subprocess.TimeoutExpired:
+                continue
+    timer = threading.Timer(args.launch_timeout, deadline)
+    timer.daemon = True
+    timer.start()
+    line = None
+    try:
+        for ln in p.stdout:
+            sys.stdout.write(ln)
+            sys.stdout.flush()
+            if ln.startswith("{"):
+                try:
+                    line = json.loads(ln)
+                except json.JSONDecodeError:
+                    pass
+        rc = p.wait()
+    finally:
+        timer.cancel()
+        if p.poll() is None:
+            deadline()
+    if expired.is_set():
+        print(f"bench.py: the {args.gpus} ranks did not finish within {args.launch_timeout:.0f} s; ended them",
+              file=sys.stderr)
+        return 124
+    if rc != 0:
+        print(f"bench.py: the ranks' launcher exited {rc}", file=sys.stderr)
+        return rc if rc > 0 else 1
+    if not line or line.get("n_gpus") != args.gpus:
+        print("bench.py: rank 0 printed no result line", file=sys.stderr)
+        return 1
+    return 0
+
+
 def main():
     args = parse()
     if args.host_leg:
         return host_leg_main(args)
     import torch
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, torch))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if args.gpus > 1 and world == 1:
-            sys.exit("bench.py: --gpus N>1 must be launched with torch.distributed.run (one rank per GPU)")
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     local = local % max(torch.cuda.device_count(), 1)  # ranks share a device only in the gloo test mode
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)

@@ -244,6 +244,9 @@ inline uint64_t recv_estimate(uint64_t total, int p) {
 //                  deadline, then ncclCommAbort; host callbacks: the caller's timeout)
 //     void abandon()   -- this rank leaves without taking part in the exchange (its
 //                  transport broke): tell the peers now where the communicator can
+//                  (in-process ranks: the shared failure flag their waits poll);
+//                  otherwise the peers' exchange ends at their own deadline (RCCL:
+//                  ncclCommAbort after it; host callbacks: the caller's timeout)
 // `h_out_base` (nullable): the caller's host array of the whole sorted output; this
 // rank's range is copied to h_out_base + goff.
 //

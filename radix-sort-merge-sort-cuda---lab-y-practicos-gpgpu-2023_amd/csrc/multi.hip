@@ -196,8 +196,9 @@ struct HipRankOps {
     int sort_piece(const uint32_t *in, uint32_t *out, size_t len) {
         const int algo = LABSORT_ALGO_AUTO;
         LCALL(labsort_sort_device(in, out, len, key_type, algo, R.ws.p, R.ws.bytes, s));
-        // AUTO ran a radix layout (its first word is the device error word)
-        if (R.nerrs < RANK_CHUNKS && len > (size_t)LABSORT_AUTO_MERGE_MAX_KEYS && len <= labsort_max_keys(LABSORT_ALGO_RADIX))
+        // every layout but the one-tile sort's starts with a device error word (radix: a
+        // look-back spin that expired; merge: a four-way block with inconsistent cuts)
+        if (R.nerrs < RANK_CHUNKS && len > labsort_tile_keys())
             MHIP(hipMemcpyAsync(as<uint32_t>(R.errs) + R.nerrs++, R.ws.p, 4, hipMemcpyDeviceToDevice, s));
         return LABSORT_OK;
     }
@@ -353,7 +354,7 @@ struct HipRankOps {
             MHIP(hipMemcpy(e, R.errs.p, R.nerrs * 4, hipMemcpyDeviceToHost));
             for (int i = 0; i < R.nerrs; ++i)
                 if (e[i]) {
-                    set_detail("a sort kernel reported a device-side error (look-back spin limit)");
+                    set_detail("a sort kernel reported a device-side error (radix look-back spin limit or merge block cuts)");
                     return LABSORT_ERR_DEVICE;
                 }
         }
@@ -392,6 +393,7 @@ struct Rccl {
     decltype(&ncclGetUniqueId) uid = nullptr;
     decltype(&ncclCommInitRankConfig) init_rank_cfg = nullptr;
     decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclCommFinalize) finalize = nullptr;  // optional: older RCCL lacks it
     decltype(&ncclCommAbort) abort = nullptr;
     decltype(&ncclCommGetAsyncError) async_err = nullptr;
     decltype(&ncclAllGather) allgather = nullptr;
@@ -414,6 +416,7 @@ struct Rccl {
         uid = (decltype(uid))dlsym(h, "ncclGetUniqueId");
         init_rank_cfg = (decltype(init_rank_cfg))dlsym(h, "ncclCommInitRankConfig");
         destroy = (decltype(destroy))dlsym(h, "ncclCommDestroy");
+        finalize = (decltype(finalize))dlsym(h, "ncclCommFinalize");
         abort = (decltype(abort))dlsym(h, "ncclCommAbort");
         async_err = (decltype(async_err))dlsym(h, "ncclCommGetAsyncError");
         allgather = (decltype(allgather))dlsym(h, "ncclAllGather");
@@ -510,6 +513,35 @@ ncclConfig_t nonblocking_config() {
     return cfg;
 }
 
+// Release communicators, the documented teardown of nonblocking ones: ncclCommFinalize on
+// each (it returns at once, ncclInProgress), each polled to ncclSuccess by the deadline
+// (the peers finalize too), then ncclCommDestroy.  One that does not settle (a peer that
+// never finalizes) is aborted instead.  The pointers are cleared.
+constexpr double COMM_TEARDOWN_MS = 10000.0;
+int rccl_release(ncclComm_t *cs, size_t k, double deadline) {
+    int st = LABSORT_OK;
+    std::vector<char> fin(k, 0);
+    for (size_t i = 0; i < k; ++i)
+        if (cs[i] && g_rccl.finalize) {
+            const ncclResult_t r = g_rccl.finalize(cs[i]);
+            fin[i] = r == ncclSuccess || r == ncclInProgress;
+            if (!fin[i] && !st) st = g_rccl.fail("ncclCommFinalize", r);
+        }
+    for (size_t i = 0; i < k; ++i) {
+        if (!cs[i]) continue;
+        const int e = fin[i] ? rccl_settle(cs[i], deadline, "ncclCommFinalize") : (g_rccl.finalize ? st : LABSORT_OK);
+        if (e || (g_rccl.finalize && !fin[i])) {
+            (void)g_rccl.abort(cs[i]);
+            if (!st) st = e ? e : LABSORT_ERR_HIP;
+        } else {
+            const ncclResult_t r = g_rccl.destroy(cs[i]);
+            if (r != ncclSuccess && r != ncclInProgress && !st) st = g_rccl.fail("ncclCommDestroy", r);
+        }
+        cs[i] = nullptr;
+    }
+    return st;
+}
+
 // grouped pairwise send/recv with every peer at once: every xGMI link of the GPU
 // carries data together (the "pairwise RCCL send/recv merge" of the north_star).  The
 // group is queued whole or not at all (ncclGroupEnd), then settled by the deadline.
@@ -588,7 +620,13 @@ struct ThreadComm {
     }
     int exchange(const uint32_t *const *send, const uint64_t *sc, uint32_t *const *recv, const uint64_t *rc) {
         int st;
-        if (rccl) return rccl_exchange(sh.comms[me], sh.p, me, s, send, sc, recv, rc, sh.deadline, &sh.failed);
+        if (rccl) {
+            // queued, then waited for here, bounded: the merge that follows issues copies that
+            // can block the host behind the stream, where a peer that left would hold it
+            // forever (ncclGroupEnd can settle before the peers' kernels have run)
+            st = rccl_exchange(sh.comms[me], sh.p, me, s, send, sc, recv, rc, sh.deadline, &sh.failed);
+            return st ? st : rccl_stream_wait(sh.comms[me], s, sh.deadline, "exchange", &sh.failed);
+        }
         // peer copies straight into each receiver's slot, on the sender's stream; the
         // receivers' streams then wait for every sender's event
         sh.rptr[me] = recv;
@@ -662,7 +700,9 @@ struct RcclComm {
         return st ? failed(st) : LABSORT_OK;
     }
     int exchange(const uint32_t *const *send, const uint64_t *sc, uint32_t *const *recv, const uint64_t *rc) {
-        const int st = rccl_exchange(o.nc, p, me, s, send, sc, recv, rc, now_ms() + o.timeout_ms);
+        const double deadline = now_ms() + o.timeout_ms;
+        int st = rccl_exchange(o.nc, p, me, s, send, sc, recv, rc, deadline);
+        if (!st) st = rccl_stream_wait(o.nc, s, deadline, "exchange");  // as ThreadComm::exchange
         return st ? failed(st) : LABSORT_OK;
     }
     void abandon() { o.abort(); }  // a transport that breaks is gone for every later sort too
@@ -749,8 +789,8 @@ void drop_comms() {
 int rccl_comms(const std::vector<int> &devs, double deadline) {
     if (!g_rccl.load()) return LABSORT_ERR_HIP;
     if (g_comm_devs == devs) return LABSORT_OK;
-    for (ncclComm_t c : g_comms)  // the device set changed: release the old communicators
-        if (c) (void)g_rccl.destroy(c);
+    // the device set changed: release the old communicators
+    (void)rccl_release(g_comms.data(), g_comms.size(), now_ms() + std::min(g_timeout_ms, COMM_TEARDOWN_MS));
     g_comms.assign(devs.size(), nullptr);
     g_comm_devs.clear();
     ncclUniqueId u;
@@ -1098,12 +1138,7 @@ int labsort_comm_init_host(labsort_comm_t *comm, int nranks, int rank, const lab
 int labsort_comm_destroy(labsort_comm_t c) {
     if (!c) return LABSORT_OK;
     int st = LABSORT_OK;
-    if (c->rc.nc) {
-        // (a nonblocking communicator may report its teardown as still in progress: not
-        // an error, its resources are released when it completes)
-        const ncclResult_t r = g_rccl.destroy(c->rc.nc);
-        if (r != ncclSuccess && r != ncclInProgress) st = g_rccl.fail("ncclCommDestroy", r);
-    }
+    if (c->rc.nc) st = rccl_release(&c->rc.nc, 1, now_ms() + std::min(c->rc.timeout_ms, COMM_TEARDOWN_MS));
     if (c->R.dev >= 0) {
         (void)hipSetDevice(c->R.dev);
         for (Buf *b : {&c->R.x, &c->R.y, &c->R.ws, &c->R.mws, &c->R.recv, &c->R.out, &c->R.small, &c->R.part,

@@ -104,7 +104,11 @@ def add_big(names, fresh=False):
         if lg <= 24:
             c = a.view(np.int32).copy()
             c.sort(kind="stable")
-            big[name]["sha256_sorted_i32"] = sha(c)
+        else:  # int32 order of the same multiset: the negative keys (top bit set) first
+            k = int(np.searchsorted(b, np.uint32(1 << 31)))
+            c = np.concatenate([b[k:], b[:k]])
+        big[name]["sha256_sorted_i32"] = sha(c)
+        del c
         print(name, big[name]["sha256_sorted_u32"][:16])
         del a, b
     with open(path, "w") as f:

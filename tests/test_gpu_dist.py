@@ -359,3 +359,37 @@ def test_bench_dist_gloo_config5():
     ph = line["xgmi"]["phases_ms_last_step"]
     assert ph["plan_work"] >= 0 and ph["plan_wait"] >= 0
     assert set(line["xgmi"]["collectives_ms_last_step"]) >= {"samples", "counts"}
+
+
+def test_bench_plain_gpus2_launches_ranks():
+    """`python3 bench.py --gpus 2` WITHOUT torch.distributed.run (how the driver invokes the
+    bench): bench.py starts the two ranks itself and relays rank 0's config-5 line"""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                        "--steps", "1", "--warmup", "0", "--no-weak", "--no-host-path", "--total-log2n", "26"],
+                       capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert "BASELINE config 5" in line["config"]["workload"]
+    assert line["config"]["n_total"] == 1 << 26 and line["value"] > 0
+
+
+def test_bench_plain_gpus8_nccl_refused_on_one_gpu():
+    """--gpus 8 over RCCL on a box with fewer GPUs: refused at once, non-zero"""
+    import subprocess
+    import time
+    import torch
+    if torch.cuda.device_count() >= 8:
+        pytest.skip("an 8-GPU box runs the real thing")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "1"],
+                       capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode != 0
+    assert time.monotonic() - t0 < 30
+    assert "needs 8 GPUs" in r.stderr

@@ -39,10 +39,11 @@ def test_fullsize_sha(ls, torch_gpu, name, algo):
     assert sha(got) == c["sha256_sorted_u32"]
 
 
-@pytest.mark.parametrize("name", ["config2_2^20_u32", "2^24_u32", "2^24_mod1000"])
+@pytest.mark.parametrize("name", ["config2_2^20_u32", "2^24_u32", "2^24_mod1000", "config3_2^28_u32"])
 @pytest.mark.parametrize("algo", ["radix", "merge"])
 def test_fullsize_sha_i32(ls, torch_gpu, name, algo):
-    """The same inputs in int32 order (sign-flipped digits and comparisons)."""
+    """The same inputs in int32 order (sign-flipped digits and comparisons): the
+    reference's own key type (lab.h:9), up to BASELINE config 3's 2^28 keys."""
     torch = torch_gpu
     c = BIG[name]
     n = 1 << c["log2n"]
@@ -186,3 +187,23 @@ def test_fullsize_host_pipeline(ls, torch_gpu, name):
     ls.sort_host(a, algo="auto")
     assert int(a[0]) == c["first"] and int(a[-1]) == c["last"] and int(a[n // 2]) == c["median"]
     assert sha(a) == c["sha256_sorted_u32"]
+
+
+def test_fullsize_order_array_i32_2e30(ls, torch_gpu):
+    """BASELINE config 5's 2^30 keys as the reference's caller passes them: a host int*
+    sorted in place by the exported order_array(int*, int) (lab.h:9, called through
+    ctypes), signed order, checked word for word against the int32 fixture."""
+    import ctypes
+    torch = torch_gpu
+    c = BIG["config5_2^30_u32"]
+    n = 1 << c["log2n"]
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, c["seed"], c["dist"])
+    a = t.cpu().numpy()
+    del t
+    torch.cuda.empty_cache()
+    fn = getattr(ls.lib, "_Z11order_arrayPii")
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    fn(a.ctypes.data, n)
+    assert sha(a) == c["sha256_sorted_i32"]

@@ -328,6 +328,22 @@ def test_order_array_negative_keys(ls, oracle, torch_gpu):
     np.testing.assert_array_equal(b, np.sort(a))
 
 
+@pytest.mark.parametrize("symbol", ["sort", "_Z11order_arrayPii"])
+@pytest.mark.parametrize("n", [1000, 65536, (1 << 20) + 3])
+def test_c_abi_sort_symbols_match_std_sort(ls, oracle, torch_gpu, symbol, n):
+    """The exported entry points themselves, called through ctypes as a C caller would:
+    the north_star's extern "C" sort(int*, int) and order_array(int*, int) (lab.h:9),
+    signed int keys, against std::sort in int32 order (the oracle)."""
+    import ctypes
+    a = oracle.gen(n, SEED + 16, "u32").view(np.int32).copy()
+    b = a.copy()
+    fn = getattr(ls.lib, symbol)
+    fn.restype = None
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    fn(b.ctypes.data, n)
+    np.testing.assert_array_equal(b, oracle.sort_i32(a))
+
+
 def test_order_with_trust(ls, oracle):
     a = oracle.gen(65536, SEED + 14, "mod1000").astype(np.int32)
     b = a.copy()
