@@ -8,6 +8,7 @@ KRE="$1"; TAG="$2"
 SETS=("SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM"
       "SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_INSTS_LDS SQ_INSTS_VALU SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE"
       "FETCH_SIZE" "WRITE_SIZE")
+[ -n "${SQ_ONLY:-}" ] && SETS=("${SETS[@]:0:2}")  # the two SQ passes only
 i=0
 for set in "${SETS[@]}"; do
   i=$((i+1))

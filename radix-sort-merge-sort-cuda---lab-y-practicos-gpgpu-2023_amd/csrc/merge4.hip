@@ -307,7 +307,13 @@ __global__ M4_RANK_LB void k_m4_rank(const uint32_t *__restrict__ src, M4Geo G, 
 }
 
 // merge-path co-rank in LDS: A elements among the first d of merge(A, B) (FLIP: int32 order).
-// r29, measured slower: a branch-free form with a workgroup-uniform number of halving steps
+// r31, measured slower (profiles/r31_ab_merge4.txt): fixed power-of-two steps with a wave-uniform
+// count (the wave's largest range, from the block geometry on scalars) and running probe
+// pointers: 10 % fewer VALU per pass, but every lane's first probes share A's word and fall
+// on B at an 8-word lane stride, and LDS bank conflicts rose 150 M -> 222 M cycles: 0.771 vs
+// 0.653 ms.  The probes of this loop (midpoints ~4 words apart across lanes, 4-way conflicts)
+// are most of the kernel's conflict cycles, and the kernel is VALU- (~80 %) and LDS- (~67 %)
+// busy at once.  r29, measured slower: a branch-free form with a workgroup-uniform number of halving steps
 // (7 VALU per step instead of 9; +0.09 ms per pass: the data-dependent loop stops early), and
 // two-step searches (the co-ranks of every 64th diagonal first, by two waves, then each thread
 // within its 64: +0.10 ms per pass from the two extra barriers per block)
@@ -325,7 +331,8 @@ __device__ __forceinline__ uint32_t m4_corank(const uint32_t *A, uint32_t la, co
 
 // 8 consecutive LDS words base[i .. i + 8) by five 8-B reads of the 10 words from i rounded
 // down to even, and one select per word (16-B reads needed three selects per word; eight 4-B
-// reads, no selects: 0.691 vs 0.687 ms per pass, r29)
+// reads, no selects: 0.691 vs 0.687 ms per pass, r29; r31 again, as four ds_read2_b32 with
+// 46 VALU fewer per block: 0.782 vs 0.771 ms, profiles/r31_ab_merge4.txt)
 __device__ __forceinline__ void m4_read8(const uint32_t *base, uint32_t i, uint32_t (&w)[M4_KPT]) {
     const uint32_t a = i & ~1u;
     const bool odd = (i & 1u) != 0u;
@@ -376,6 +383,7 @@ __device__ __forceinline__ void m4_window_merge(const uint32_t *buf, uint32_t A,
 }
 
 constexpr uint32_t M4_PAD = M4_KPT;  // +inf words after every run in LDS
+static_assert((M4_M + 3) * M4_S + 4 * M4_PAD <= M4_CAP, "a block's padded LDS image fits one load pass of the threads");
 // buf[p]: a block's keys A | pad | B | pad | C | pad | D | pad, then its output staging;
 // buf[1 - p]: level 1's A+B | pad | C+D | pad, then the next block's keys (p alternates)
 constexpr uint32_t M4_BUFW = M4_CAP + 4 * M4_PAD + 16;
@@ -421,7 +429,7 @@ __device__ __forceinline__ M4Blk m4_block(const M4Geo &G, const uint4 *lo, uint3
     // labsort_workspace_status reports as LABSORT_ERR_DEVICE)
     q.bad = 0u;
     if (h4.x < l4.x || h4.y < l4.y || h4.z < l4.z || h4.w < l4.w || h4.x > rl[0] || h4.y > rl[1] || h4.z > rl[2] ||
-        h4.w > rl[3] || q.tot > M4_CAP - 2 * M4_KPT) {
+        h4.w > rl[3] || q.tot > M4_CAP - 4 * M4_PAD) {
         q.tot = 0u;
         q.bad = 1u;
 #pragma unroll
@@ -446,37 +454,40 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
     const uint32_t b0 = blockIdx.x * per;
     if (b0 >= G.nblocks) return;
     const uint32_t b1 = b0 + per < G.nblocks ? b0 + per : G.nblocks;
-    // keys of block q into registers: element tid + j BLOCK of the windows A | B | C | D, at a
-    // 32-bit offset from the group's base (one select of a uniform delta per window boundary,
-    // a saddr load); elements past the block carry +inf (they become D's pads in LDS)
+    // block q's LDS image into registers, by LDS position: position p = tid + j BLOCK of
+    // A | pad | B | pad | C | pad | D | pad (window k at S_k, its keys at a 32-bit offset
+    // delta_k + p from the group's base; the pads and everything past D hold +inf), so the
+    // store into LDS is one write per word at a fixed offset (r31: the put's per-word LDS
+    // shifts and pad writes were ~12 % of the kernel's VALU; a wave-uniform fast path for
+    // chunks inside one window, tested on scalars, measured slower: 0.757 vs 0.680 ms)
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(tid) & ~63u, lane = tid & 63u;
     auto load = [&](const M4Blk &q, uint32_t (&v)[M4_KPT]) {
-        const uint32_t o1 = q.len[0], o2 = o1 + q.len[1], o3 = o2 + q.len[2];
-        const char *gb = reinterpret_cast<const char *>(src + (size_t)q.g * 4u * G.r);
-        const uint32_t d0 = q.lo[0], d1 = G.r + q.lo[1] - o1, d2 = 2u * G.r + q.lo[2] - o2, d3 = 3u * G.r + q.lo[3] - o3;
+        const uint32_t S1 = q.len[0] + M4_PAD, S2 = S1 + q.len[1] + M4_PAD, S3 = S2 + q.len[2] + M4_PAD;
+        const uint32_t E0 = q.len[0], E1 = S1 + q.len[1], E2 = S2 + q.len[2], E3 = S3 + q.len[3];
+        const uint32_t D0 = q.lo[0], D1 = G.r + q.lo[1] - S1, D2 = 2u * G.r + q.lo[2] - S2, D3 = 3u * G.r + q.lo[3] - S3;
+        const uint32_t *gbase = src + (size_t)q.g * 4u * G.r;
+        // the selected values held in VGPRs once per block: as scalars every select of the
+        // chains below needed a v_mov of its operand first (one scalar operand per VALU op)
+        uint32_t e[4] = {E0, E1, E2, E3}, dl[4] = {D0, D1, D2, D3};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            asm("" : "+v"(e[w]));
+            asm("" : "+v"(dl[w]));
+        }
 #pragma unroll
         for (int j = 0; j < M4_KPT; ++j) {
-            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
-            uint32_t dd = d0;
-            dd = i >= o1 ? d1 : dd;
-            dd = i >= o2 ? d2 : dd;
-            dd = i >= o3 ? d3 : dd;
-            const size_t off = WIDE ? (size_t)(i + dd) * 4u : (size_t)(uint32_t)((i + dd) * 4u);
-            v[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(gb + off)) : PADV;
+            const uint32_t p = wbase + lane + (uint32_t)j * M4_BLOCK;
+            const uint32_t ee = p >= S3 ? e[3] : p >= S2 ? e[2] : p >= S1 ? e[1] : e[0];
+            const uint32_t d = p >= S3 ? dl[3] : p >= S2 ? dl[2] : p >= S1 ? dl[1] : dl[0];
+            // (a saddr load at a 32-bit byte offset unless the group's bytes pass 2^32)
+            const size_t off = WIDE ? (size_t)(p + d) * 4u : (size_t)(uint32_t)((p + d) * 4u);
+            v[j] = p < ee ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(reinterpret_cast<const char *>(gbase) + off))
+                         : PADV;
         }
     };
-    // block q's keys (registers v) into X with a pad of +inf after each window
-    auto put = [&](uint32_t *X, const M4Blk &q, const uint32_t (&v)[M4_KPT]) {
-        const uint32_t la = q.len[0], lab = la + q.len[1], labc = lab + q.len[2];
+    auto put = [&](uint32_t *X, const uint32_t (&v)[M4_KPT]) {
 #pragma unroll
-        for (int j = 0; j < M4_KPT; ++j) {
-            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
-            const uint32_t sh = (i >= la ? M4_PAD : 0u) + (i >= lab ? M4_PAD : 0u) + (i >= labc ? M4_PAD : 0u);
-            X[i + sh] = v[j];  // (past the block: +inf, D's pads first)
-        }
-        if (tid < 3u * M4_PAD) {  // A's, B's and C's pads
-            const uint32_t k = tid / M4_PAD, e = tid % M4_PAD;
-            X[(k == 0 ? la : k == 1 ? lab + M4_PAD : labc + 2u * M4_PAD) + e] = PADV;
-        }
+        for (int j = 0; j < M4_KPT; ++j) X[wbase + lane + (uint32_t)j * M4_BLOCK] = v[j];
     };
     // the start cuts of blocks b0 .. b1 (a group's first block starts at 0) into LDS: one
     // global round trip here instead of one before every block's key loads
@@ -488,7 +499,7 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
     uint32_t nx[M4_KPT];
     M4Blk cur = m4_block(G, sm.lo, b0, 0u);
     load(cur, nx);
-    put(sm.buf[0], cur, nx);
+    put(sm.buf[0], nx);
     M4Blk nxt = cur;
     if (b0 + 1u < b1) {
         nxt = m4_block(G, sm.lo, b0 + 1u, 1u);
@@ -560,7 +571,7 @@ __global__ __launch_bounds__(M4_BLOCK, 8) void k_m4_merge(const uint32_t *__rest
         }
         // the next block's keys into Y (its X), and the one after into registers
         if (id + 1u < b1) {
-            put(Y, nxt, nx);
+            put(Y, nx);
             cur = nxt;
             if (id + 2u < b1) {
                 nxt = m4_block(G, sm.lo, id + 2u, id + 2u - b0);
@@ -631,33 +642,36 @@ __global__ __launch_bounds__(M4_BLOCK, 4) void k_m4_merge_kv(const uint32_t *__r
     const uint32_t b0 = blockIdx.x * per;
     if (b0 >= G.nblocks) return;
     const uint32_t b1 = b0 + per < G.nblocks ? b0 + per : G.nblocks;
-    // keys and payloads of block q into registers (as k_m4_merge; no +inf fill: the
-    // key/value merges check their bounds)
+    // keys and payloads of block q into registers by LDS position, as k_m4_merge (no +inf
+    // pads: the key/value merges check their bounds, so pad positions load nothing)
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(tid) & ~63u, lane = tid & 63u;
     auto load = [&](const M4Blk &q, uint32_t (&v)[M4_KPT], uint32_t (&pl)[M4_KPT]) {
-        const uint32_t o1 = q.len[0], o2 = o1 + q.len[1], o3 = o2 + q.len[2];
+        const uint32_t S1 = q.len[0] + M4_PAD, S2 = S1 + q.len[1] + M4_PAD, S3 = S2 + q.len[2] + M4_PAD;
+        uint32_t e[4] = {q.len[0], S1 + q.len[1], S2 + q.len[2], S3 + q.len[3]};
+        uint32_t dl[4] = {q.lo[0], G.r + q.lo[1] - S1, 2u * G.r + q.lo[2] - S2, 3u * G.r + q.lo[3] - S3};
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // (held in VGPRs: see k_m4_merge)
+            asm("" : "+v"(e[w]));
+            asm("" : "+v"(dl[w]));
+        }
         const size_t gofs = (size_t)q.g * 4u * G.r;
         const char *gb = reinterpret_cast<const char *>(src + gofs), *vb = reinterpret_cast<const char *>(vsrc + gofs);
-        const uint32_t d0 = q.lo[0], d1 = G.r + q.lo[1] - o1, d2 = 2u * G.r + q.lo[2] - o2, d3 = 3u * G.r + q.lo[3] - o3;
 #pragma unroll
         for (int j = 0; j < M4_KPT; ++j) {
-            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
-            uint32_t dd = d0;
-            dd = i >= o1 ? d1 : dd;
-            dd = i >= o2 ? d2 : dd;
-            dd = i >= o3 ? d3 : dd;
-            const size_t off = WIDE ? (size_t)(i + dd) * 4u : (size_t)(uint32_t)((i + dd) * 4u);
-            v[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(gb + off)) : 0u;
-            pl[j] = i < q.tot ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(vb + off)) : 0u;
+            const uint32_t p = wbase + lane + (uint32_t)j * M4_BLOCK;
+            const uint32_t ee = p >= S3 ? e[3] : p >= S2 ? e[2] : p >= S1 ? e[1] : e[0];
+            const uint32_t d = p >= S3 ? dl[3] : p >= S2 ? dl[2] : p >= S1 ? dl[1] : dl[0];
+            const size_t off = WIDE ? (size_t)(p + d) * 4u : (size_t)(uint32_t)((p + d) * 4u);
+            const bool ok = p < ee;
+            v[j] = ok ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(gb + off)) : 0u;
+            pl[j] = ok ? ld_stream<NT_MERGE>(reinterpret_cast<const uint32_t *>(vb + off)) : 0u;
         }
     };
-    auto put = [&](uint32_t *X, uint32_t *XV, const M4Blk &q, const uint32_t (&v)[M4_KPT], const uint32_t (&pl)[M4_KPT]) {
-        const uint32_t la = q.len[0], lab = la + q.len[1], labc = lab + q.len[2];
+    auto put = [&](uint32_t *X, uint32_t *XV, const uint32_t (&v)[M4_KPT], const uint32_t (&pl)[M4_KPT]) {
 #pragma unroll
         for (int j = 0; j < M4_KPT; ++j) {
-            const uint32_t i = tid + (uint32_t)j * M4_BLOCK;
-            const uint32_t sh = (i >= la ? M4_PAD : 0u) + (i >= lab ? M4_PAD : 0u) + (i >= labc ? M4_PAD : 0u);
-            X[i + sh] = v[j];
-            XV[i + sh] = pl[j];
+            X[wbase + lane + (uint32_t)j * M4_BLOCK] = v[j];
+            XV[wbase + lane + (uint32_t)j * M4_BLOCK] = pl[j];
         }
     };
     for (uint32_t t = tid; t <= b1 - b0; t += M4_BLOCK) {
@@ -668,7 +682,7 @@ __global__ __launch_bounds__(M4_BLOCK, 4) void k_m4_merge_kv(const uint32_t *__r
     uint32_t nx[M4_KPT], nv[M4_KPT];
     M4Blk cur = m4_block(G, sm.lo, b0, 0u);
     load(cur, nx, nv);
-    put(sm.buf[0], sm.vbuf[0], cur, nx, nv);
+    put(sm.buf[0], sm.vbuf[0], nx, nv);
     M4Blk nxt = cur;
     if (b0 + 1u < b1) {
         nxt = m4_block(G, sm.lo, b0 + 1u, 1u);
@@ -735,7 +749,7 @@ __global__ __launch_bounds__(M4_BLOCK, 4) void k_m4_merge_kv(const uint32_t *__r
             }
         }
         if (id + 1u < b1) {
-            put(Y, YV, nxt, nx, nv);
+            put(Y, YV, nx, nv);
             cur = nxt;
             if (id + 2u < b1) {
                 nxt = m4_block(G, sm.lo, id + 2u, id + 2u - b0);

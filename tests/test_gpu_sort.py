@@ -173,6 +173,25 @@ def test_merge_four_way_shapes(ls, oracle, torch_gpu, n, dist):
         np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key), err_msg=f"{key}")
 
 
+@pytest.mark.parametrize("m", list(range(1, 17)))
+def test_merge_four_way_short_last_run(ls, oracle, torch_gpu, m):
+    """n = m * 32768 + L for L in {1, 127, 128, 129}: the last group of every four-way pass
+    (runs of 32768, 65536, 131072 keys, after a pairwise pass or not) ends in a run of one
+    key, just under / exactly / just over one sample stride (M4_S = 128), at each of the four
+    run positions as m varies, with the group's later runs empty: the rank kernel's sample
+    counts and the cut rounds' clamps (merge4.hip m4_cut_round) at their edges."""
+    torch = torch_gpu
+    for L in (1, 127, 128, 129):
+        n = m * 32768 + L
+        a = oracle.gen(n, SEED + 60 + m * 7 + L, "u32")
+        t = to_dev(torch, a)
+        o = torch.empty_like(t)
+        for key in ("u32", "i32"):
+            ls.sort_device(t, o, n, key=key, algo="merge")
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(from_dev(o), ref_sort(oracle, a, key), err_msg=f"n={n} {key}")
+
+
 # ---- merge building blocks ------------------------------------------------------------------
 def test_merge_pass(ls, oracle, torch_gpu):
     torch = torch_gpu
