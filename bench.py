@@ -582,7 +582,15 @@ def launch_ranks(args, torch) -> int:
     env["PYTHONUNBUFFERED"] = "1"
     cmd = [sys.executable, "-u", "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
-    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True)
+    def on_parent_death():  # (in the child: if this launcher is killed, torch.distributed.run gets SIGTERM
+        # and ends its ranks, instead of leaving them on the GPUs)
+        try:
+            import ctypes
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True,
+                         preexec_fn=on_parent_death)
     expired = threading.Event()
 
     def deadline():
