@@ -333,13 +333,14 @@ __device__ __forceinline__ uint32_t m4_corank(const uint32_t *A, uint32_t la, co
 // down to even, and one select per word (16-B reads needed three selects per word; eight 4-B
 // reads, no selects: 0.691 vs 0.687 ms per pass, r29; r31 again, as four ds_read2_b32 with
 // 46 VALU fewer per block: 0.782 vs 0.771 ms, profiles/r31_ab_merge4.txt)
-__device__ __forceinline__ void m4_read8(const uint32_t *base, uint32_t i, uint32_t (&w)[M4_KPT]) {
+template <int W = M4_KPT>
+__device__ __forceinline__ void m4_read8(const uint32_t *base, uint32_t i, uint32_t (&w)[W]) {
     const uint32_t a = i & ~1u;
     const bool odd = (i & 1u) != 0u;
     const uint2 *p = reinterpret_cast<const uint2 *>(base + a);
-    uint32_t b[M4_KPT + 2];
+    uint32_t b[W + 2];
 #pragma unroll
-    for (int q = 0; q < M4_KPT / 2 + 1; ++q) {
+    for (int q = 0; q < W / 2 + 1; ++q) {
         const uint2 v = p[q];
         b[2 * q] = v.x;
         b[2 * q + 1] = v.y;
@@ -348,29 +349,29 @@ __device__ __forceinline__ void m4_read8(const uint32_t *base, uint32_t i, uint3
     // the scratch stack)
     const uint32_t m = odd ? 0xFFFFFFFFu : 0u;
 #pragma unroll
-    for (int j = 0; j < M4_KPT; ++j) w[j] = (b[j] & ~m) | (b[j + 1] & m);
+    for (int j = 0; j < W; ++j) w[j] = (b[j] & ~m) | (b[j + 1] & m);
 }
 
-// the 8 smallest of A[ai, ai + 8) and B[bi, bi + 8), by a bitonic merge of A ascending with B
-// descending.  A and B are LDS word offsets into `buf` (8-B aligned); each run is followed by
-// 8 pad words of +inf, so the windows need no bounds (equal keys are identical words: a pad
-// equal to a key changes no output).
-template <bool FLIP>
+// the W smallest of A[ai, ai + W) and B[bi, bi + W), by a bitonic merge of A ascending with B
+// descending (only the lower half of the network is kept).  A and B are LDS word offsets into
+// `buf` (8-B aligned); each run is followed by W pad words of +inf, so the windows need no
+// bounds (equal keys are identical words: a pad equal to a key changes no output).
+template <bool FLIP, int W = M4_KPT>
 __device__ __forceinline__ void m4_window_merge(const uint32_t *buf, uint32_t A, uint32_t ai, uint32_t B, uint32_t bi,
-                                                uint32_t (&r)[M4_KPT]) {
+                                                uint32_t (&r)[W]) {
     constexpr uint32_t flip = FLIP ? 0x80000000u : 0u;
-    uint32_t wa[M4_KPT], wb[M4_KPT], x[2 * M4_KPT];
-    m4_read8(buf, A + ai, wa);
-    m4_read8(buf, B + bi, wb);
+    uint32_t wa[W], wb[W], x[2 * W];
+    m4_read8<W>(buf, A + ai, wa);
+    m4_read8<W>(buf, B + bi, wb);
 #pragma unroll
-    for (int j = 0; j < M4_KPT; ++j) {
+    for (int j = 0; j < W; ++j) {
         x[j] = wa[j] ^ flip;
-        x[2 * M4_KPT - 1 - j] = wb[j] ^ flip;
+        x[2 * W - 1 - j] = wb[j] ^ flip;
     }
 #pragma unroll
-    for (int s = M4_KPT; s >= 1; s >>= 1) {
+    for (int s = W; s >= 1; s >>= 1) {
 #pragma unroll
-        for (int i = 0; i < 2 * M4_KPT; ++i) {
+        for (int i = 0; i < 2 * W; ++i) {
             if ((i & s) == 0) {
                 const uint32_t lo = min(x[i], x[i + s]), hi = max(x[i], x[i + s]);
                 x[i] = lo;
@@ -379,8 +380,12 @@ __device__ __forceinline__ void m4_window_merge(const uint32_t *buf, uint32_t A,
         }
     }
 #pragma unroll
-    for (int j = 0; j < M4_KPT; ++j) r[j] = x[j] ^ flip;
+    for (int j = 0; j < W; ++j) r[j] = x[j] ^ flip;
 }
+
+// (r31: level 2 at 16 outputs per thread -- half that level's co-rank searches, by the first
+// 256 threads, with 16-word pads after A+B and C+D -- needs 18 VGPRs of spills at the kernel's
+// 64-register budget: 1.097 vs 0.660 ms, profiles/r31_ab_merge4.txt)
 
 constexpr uint32_t M4_PAD = M4_KPT;  // +inf words after every run in LDS
 static_assert((M4_M + 3) * M4_S + 4 * M4_PAD <= M4_CAP, "a block's padded LDS image fits one load pass of the threads");
