@@ -339,6 +339,8 @@ def host_leg_main(args) -> None:
         out[f"error_{args.host_leg}"] = f"{torch.cuda.device_count()} devices visible, {args.gpus} needed"
     elif args.gpus > 1:
         devs = list(range(args.gpus))
+        if args.host_leg == "rccl":
+            ls.set_comm_timeout(30.0)  # (a transport problem ends this leg in 30 s, well inside its 100 s limit)
         try:
             el, ok = timed(lambda a: ls.sort_host_ranks(a, devs, transport=args.host_leg), 3)
         except ls.LabsortError as e:
