@@ -317,22 +317,30 @@ __global__ M4_RANK_LB void k_m4_rank(const uint32_t *__restrict__ src, M4Geo G, 
 // (7 VALU per step instead of 9; +0.09 ms per pass: the data-dependent loop stops early), and
 // two-step searches (the co-ranks of every 64th diagonal first, by two waves, then each thread
 // within its 64: +0.10 ms per pass from the two extra barriers per block)
+typedef __attribute__((address_space(3))) const uint32_t m4_lds_u32;
+__device__ __forceinline__ uint32_t m4_lds_addr(const uint32_t *p) { return (uint32_t)(uintptr_t)(m4_lds_u32 *)p; }
+__device__ __forceinline__ uint32_t m4_lds_ld(uint32_t a) { return *(m4_lds_u32 *)(uintptr_t)a; }
+// (r31) the bounds are kept as LDS byte addresses of A: the midpoint's address is
+// ((lo + hi) / 2) & ~3 and its B partner one subtraction away (B[d - 1 - mid] at bk - mid):
+// 9 VALU per step instead of 10, the same probes (0.718 -> 0.709 ms per four-way pass)
 template <bool FLIP>
 __device__ __forceinline__ uint32_t m4_corank(const uint32_t *A, uint32_t la, const uint32_t *B, uint32_t lb, uint32_t d) {
     constexpr uint32_t flip = FLIP ? 0x80000000u : 0u;
-    uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if ((A[mid] ^ flip) <= (B[d - 1u - mid] ^ flip)) lo = mid + 1u;
-        else hi = mid;
+    const uint32_t lo = d > lb ? d - lb : 0u, hi = d < la ? d : la;
+    const uint32_t a0 = m4_lds_addr(A), bk = m4_lds_addr(B) + 4u * (d - 1u) + a0;
+    uint32_t lob = a0 + 4u * lo, hib = a0 + 4u * hi;
+    while (lob < hib) {
+        const uint32_t midb = ((lob + hib) >> 1) & ~3u;
+        if ((m4_lds_ld(midb) ^ flip) <= (m4_lds_ld(bk - midb) ^ flip)) lob = midb + 4u;
+        else hib = midb;
     }
-    return lo;
+    return (lob - a0) >> 2;
 }
 
 // 8 consecutive LDS words base[i .. i + 8) by five 8-B reads of the 10 words from i rounded
 // down to even, and one select per word (16-B reads needed three selects per word; eight 4-B
 // reads, no selects: 0.691 vs 0.687 ms per pass, r29; r31 again, as four ds_read2_b32 with
-// 46 VALU fewer per block: 0.782 vs 0.771 ms, profiles/r31_ab_merge4.txt)
+// 46 VALU fewer per block: 0.782 vs 0.771 ms and 0.7138 vs 0.7089 ms, profiles/r31_ab_merge4.txt)
 template <int W = M4_KPT>
 __device__ __forceinline__ void m4_read8(const uint32_t *base, uint32_t i, uint32_t (&w)[W]) {
     const uint32_t a = i & ~1u;
