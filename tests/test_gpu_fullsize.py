@@ -106,6 +106,47 @@ def test_fullsize_past_2e30_merge(ls, torch_gpu, key, n):
     assert fp(t) == fp(o)
 
 
+def _props(ls, torch, t, o, n, key):
+    """(descents of o, equal digit histograms, equal sum / sum of squares): o is t sorted"""
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    ls.count_descents(o, n, cnt, key=key)
+    hs = torch.zeros(4 * 256, dtype=torch.int32, device="cuda")
+    ho = torch.zeros(4 * 256, dtype=torch.int32, device="cuda")
+    ls.histogram(t, n, hs, bits=8, key=key)
+    ls.histogram(o, n, ho, bits=8, key=key)
+
+    def fp(x):
+        s1 = s2 = 0
+        for part in torch.split(x, 1 << 26):
+            v = part.to(torch.int64) & 0xFFFFFFFF
+            s1 += int(v.sum().item())
+            s2 = (s2 + int((v * v).sum().item())) & (2**64 - 1)
+        return s1, s2
+
+    return int(cnt.item()), torch.equal(hs, ho), fp(t) == fp(o)
+
+
+@pytest.mark.parametrize("dist,param", [("sorted", 0), ("reversed", 0), ("const", 0x8000_0001), ("mod100", 0),
+                                        ("lowbits", 3), ("u31", 0)])
+@pytest.mark.parametrize("algo", ["radix", "merge"])
+@pytest.mark.parametrize("key", ["u32", "i32"])
+def test_fullsize_distributions(ls, torch_gpu, dist, param, algo, key):
+    """BASELINE config 3/4's size (2^28 keys) on the non-uniform shapes the reference's
+    harness and tests exercise at small n (sorted, reversed, constant, few distinct keys,
+    u31 = main.cpp's rand()): the onesweep passes' skipped digits and single-chain plans,
+    the four-way pass's blocks made of one run and its equal keys across runs.  Checked by
+    size-independent properties against the input (no fixture holds these outputs)."""
+    torch = torch_gpu
+    n = 1 << 28
+    t = torch.empty(n, dtype=torch.int32, device="cuda")
+    ls.fill(t, n, 0x5EED0041, dist, param=param)
+    o = torch.empty_like(t)
+    ls.sort_device(t, o, n, key=key, algo=algo)
+    torch.cuda.synchronize()
+    desc, hist_eq, fp_eq = _props(ls, torch, t, o, n, key)
+    assert desc == 0 and hist_eq and fp_eq
+
+
 def test_fullsize_past_2e30_merge_pairs(ls, torch_gpu):
     """Key/value merge sort of 2^30 + 4097 (key, index) pairs: the key/value four-way
     pass's 64-bit offsets.  Checked chunk by chunk: keys without descent, every payload's
