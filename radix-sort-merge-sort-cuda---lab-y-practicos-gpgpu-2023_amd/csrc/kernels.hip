@@ -404,19 +404,24 @@ __device__ void build_segplan_later(SegPlan *__restrict__ out, int q, uint32_t p
 // buffers; plus each pass's next active digit) and every active pass's SegPlan (the
 // later passes' plans depend only on the histograms, so they are built here, not by
 // a launch before each pass).
-// Workgroups 1.. clear the look-back region (zp, zn4 uint4s) while workgroup 0 builds the
-// plans: one launch instead of a k_zero launch and this one (the look-back words are
-// only read by the passes after it).
+// Workgroups 0-3 each derive the whole pass structure from the histograms (a few us of
+// redundant reads) and workgroup q builds pass q's SegPlan, so the four plans are built at
+// once (r31: one workgroup building them in turn took 18.7 us per sort); workgroup 0 also
+// writes the Plan.  Workgroups 4.. clear the look-back region (zp, zn4 uint4s): one launch
+// instead of a k_zero launch and this one (the look-back words are only read by the
+// passes after it).
 __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps, const uint32_t *__restrict__ joint,
                                                uint32_t n, int in_is_out, int seg_later, Plan *__restrict__ plan,
                                                SegPlan *__restrict__ sps, uint32_t *__restrict__ hist_out,
                                                uint4 *__restrict__ zp, size_t zn4) {
-    if (blockIdx.x > 0) {
-        const size_t stride = (size_t)(gridDim.x - 1) * blockDim.x;
-        for (size_t i = (size_t)(blockIdx.x - 1) * blockDim.x + threadIdx.x; i < zn4; i += stride)
+    constexpr uint32_t PW = 4;  // plan workgroups, one per pass
+    if (blockIdx.x >= PW) {
+        const size_t stride = (size_t)(gridDim.x - PW) * blockDim.x;
+        for (size_t i = (size_t)(blockIdx.x - PW) * blockDim.x + threadIdx.x; i < zn4; i += stride)
             zp[i] = make_uint4(0u, 0u, 0u, 0u);
         return;
     }
+    const int me = (int)blockIdx.x;  // the pass whose SegPlan this workgroup builds
     __shared__ uint32_t hist[4 * 256];
     __shared__ uint32_t sh[NSEG * 256 + 8];
     __shared__ uint32_t triv[4];
@@ -435,12 +440,24 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
         hist[p * 256 + t] = v[p];
-        hist_out[p * 256 + t] = v[p];
+        if (me == 0) hist_out[p * 256 + t] = v[p];
         if (v[p] == n) triv[p] = 1;
     }
     if (t <= (uint32_t)NSEG) start[t] = seg_later < 0 ? (t ? n : 0u) : seg_start(t, n);
     __syncthreads();
-    if (t == 0) {
+    if (t == 0 && me != 0) {  // the pass structure only
+        int k = 0, last = -1;
+        for (int p = 0; p < 4; ++p) {
+            prevs[p] = NEXT_NONE;
+            if (!triv[p]) {
+                if (last >= 0) prevs[p] = (uint32_t)last;
+                last = p;
+                if (!k++) first = p;
+            }
+        }
+        if (!k) first = -1;
+    }
+    if (t == 0 && me == 0) {
         int act[4];
         int k = 0;
         for (int p = 0; p < MAX_PASSES; ++p) {
@@ -481,8 +498,13 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
         }
     }
     __syncthreads();
-    if (first < 0) return;
+    if (first < 0 || me < first) return;
     // first active pass: position segments when it is digit 0 (hps), else one chain
+    if (me != first) {
+        if (prevs[me] != NEXT_NONE)  // (block-uniform) a later active pass
+            build_segplan_later(sps + me, me, prevs[me], n, seg_later, hist, joint, sh, start);
+        return;
+    }
     if (seg_later < 0 || first != 0) {
         if (t <= (uint32_t)NSEG) start[t] = t ? n : 0u;
         for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = s ? 0u : hist[first * 256 + t];
@@ -492,12 +514,6 @@ __global__ __launch_bounds__(256) void k_plan8(const uint32_t *__restrict__ hps,
         for (int s = 0; s < NSEG; ++s) sh[s * 256 + t] = hps[s * 256 + t];
         __syncthreads();
         build_segplan(sps + first, sh, start, 0u, sh);
-    }
-    // the later active passes
-    for (int q = first + 1; q < 4; ++q) {
-        if (prevs[q] == NEXT_NONE) continue;  // (block-uniform)
-        __syncthreads();  // sh, start reused
-        build_segplan_later(sps + q, q, prevs[q], n, seg_later, hist, joint, sh, start);
     }
 }
 
@@ -1814,7 +1830,7 @@ hipError_t launch_plan8(const uint32_t *hps, const uint32_t *joint, size_t n, in
         if (z != hipSuccess) return z;
     }
     const size_t zn4 = fold ? zero_bytes / 16 : 0;
-    const unsigned g = 1u + (zn4 ? blocks_for(zn4, 256 * 4, 2048) : 0u);
+    const unsigned g = 4u + (zn4 ? blocks_for(zn4, 256 * 4, 2048) : 0u);
     k_plan8<<<g, 256, 0, s>>>(hps, joint, (uint32_t)n, in_is_out, 1, plan, segplans, hist,
                               static_cast<uint4 *>(zero_p), zn4);
     return hipGetLastError();
