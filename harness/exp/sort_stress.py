@@ -1,7 +1,8 @@
 """Randomized end-to-end check of every sort entry point against numpy: device sorts by
 radix (each implementation: the size's default, LABSORT_RADIX_IMPL=onesweep / gather),
 merge and AUTO; key/value sorts (stable: payload = input index); host-pointer
-sorts (order_array's path, pipelined from 2^27 keys only, so here the single-shot path).
+sorts (order_array's path, pipelined from 2^27 keys); with RANKS=1 also the multi-GPU
+schedule with 2-8 ranks sharing one GPU (labsort_sort_host_ranks, peer copies).
 Sizes log-uniform from 0 to 2^25 plus edge sizes (0, 1, powers of two +-1, tile and
 sample multiples), in place or not, u32 / i32 order, adversarial key shapes.  One line
 per failure and a summary; exit 1 on any failure.
@@ -53,7 +54,7 @@ def keys(n, shape):
 
 SHAPES = ["uniform", "u31", "few", "byte", "sorted", "reversed", "const", "extremes", "runs"]
 MODES = ["radix", "radix:onesweep", "radix:gather", "merge", "auto", "pairs:radix", "pairs:merge",
-         "host:radix", "host:merge"]
+         "host:radix", "host:merge"] + (["ranks:peer"] if os.environ.get("RANKS") else [])
 bad = 0
 counts = {}
 t0 = time.time()
@@ -89,6 +90,12 @@ for c in range(cases):
             torch.cuda.synchronize()
             perm = np.argsort(a.view(vt), kind="stable").astype(np.int32)
             ok = np.array_equal(ko.cpu().numpy().view(vt), exp) and np.array_equal(vo.cpu().numpy(), perm)
+        elif kind == "ranks":  # the multi-GPU schedule with p ranks sharing this GPU (peer copies)
+            p = int(rng.integers(2, 9))
+            h = a.view(vt).copy()
+            ls.sort_host_ranks(h, [0] * p, transport=impl)
+            ok = np.array_equal(h, exp)
+            mode = f"ranks:{impl}:p{p}"
         else:  # host pointer
             h = a.view(vt).copy()
             ls.sort_host(h, algo=impl)
